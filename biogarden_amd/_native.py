@@ -1,0 +1,178 @@
+"""ctypes binding of libbiogarden_gpu.so (include/biogarden_gpu.h).
+
+The product path: every alignment goes through this library's HIP kernels.  There is no CPU
+fallback — if the library or a GPU is missing, calls raise NativeUnavailable.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libbiogarden_gpu.so")
+
+BG_GLOBAL, BG_LOCAL, BG_FITTING, BG_OVERLAP, BG_SEMIGLOBAL = range(5)
+MODES = {"global": BG_GLOBAL, "local": BG_LOCAL, "fitting": BG_FITTING,
+         "overlap": BG_OVERLAP, "semiglobal": BG_SEMIGLOBAL}
+BG_OK, BG_INVALID_ARGUMENT_RANGE, BG_INVALID_INPUT_SIZE, BG_UNSCORABLE, BG_REF_DIVERGENT = range(5)
+BG_BLOSUM62, BG_PAM250, BG_UNIT = range(3)
+
+# every symbol include/biogarden_gpu.h declares (checked by tests/test_abi.py)
+EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align",
+           "bg_align_batch", "bg_batch_prepare", "bg_batch_execute", "bg_batch_fetch",
+           "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
+           "bg_abi_version"]
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class BgScoring(ctypes.Structure):
+    _fields_ = [("alphabet_size", ctypes.c_int32), ("code", ctypes.c_uint8 * 256),
+                ("table", ctypes.c_int32 * 1024)]
+
+
+class BgPairResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("score", ctypes.c_int32),
+                ("offset", ctypes.c_uint64), ("len", ctypes.c_uint32),
+                ("end_i", ctypes.c_uint32), ("end_j", ctypes.c_uint32),
+                ("start1", ctypes.c_uint32), ("start2", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class BgStats(ctypes.Structure):
+    _fields_ = [("cells", ctypes.c_uint64), ("trace_bytes", ctypes.c_uint64),
+                ("boundary_bytes", ctypes.c_uint64), ("residue_bytes", ctypes.c_uint64),
+                ("device_bytes", ctypes.c_uint64), ("R", ctypes.c_int32),
+                ("waves", ctypes.c_int32), ("affine", ctypes.c_int32), ("dna", ctypes.c_int32),
+                ("local", ctypes.c_int32), ("npairs", ctypes.c_int32),
+                ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float)]
+
+
+_LIB = None
+
+
+def lib():
+    """Loads the HIP library; raises NativeUnavailable when it is not built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise NativeUnavailable(
+            "libbiogarden_gpu.so is not built (run __graft_entry__.build() or make -C "
+            "biogarden_amd/csrc)")
+    L = ctypes.CDLL(LIB_PATH)
+    c_u8p = ctypes.POINTER(ctypes.c_uint8)
+    L.bg_scoring_builtin.argtypes = [ctypes.c_int, ctypes.POINTER(BgScoring)]
+    L.bg_aligner_new.argtypes = [ctypes.c_int]
+    L.bg_aligner_new.restype = ctypes.c_void_p
+    L.bg_aligner_free.argtypes = [ctypes.c_void_p]
+    L.bg_aligner_free.restype = None
+    L.bg_align.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
+                           ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(BgScoring),
+                           ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                           ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
+                           ctypes.POINTER(ctypes.c_size_t)]
+    batch_args = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t,
+                  ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                  ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                  ctypes.POINTER(BgScoring), ctypes.c_int32, ctypes.c_int32]
+    L.bg_align_batch.argtypes = batch_args + [ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
+                                              ctypes.c_size_t]
+    L.bg_batch_prepare.argtypes = batch_args
+    L.bg_batch_execute.argtypes = [ctypes.c_void_p]
+    L.bg_synchronize.argtypes = [ctypes.c_void_p]
+    L.bg_batch_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
+                                 ctypes.c_size_t]
+    L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
+    L.bg_set_tuning.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    L.bg_status_string.argtypes = [ctypes.c_int]
+    L.bg_status_string.restype = ctypes.c_char_p
+    L.bg_abi_version.restype = ctypes.c_int
+    _LIB = L
+    return L
+
+
+def builtin_scoring(which):
+    sc = BgScoring()
+    rc = lib().bg_scoring_builtin(which, ctypes.byref(sc))
+    if rc != 0:
+        raise ValueError("unknown built-in table %r" % which)
+    return sc
+
+
+def check(rc):
+    if rc < 0:
+        raise RuntimeError("biogarden_gpu: %s (%d)" % (lib().bg_status_string(rc).decode(), rc))
+    return rc
+
+
+class Handle:
+    """One bg_aligner (device scratch arenas + HIP stream) on one GPU."""
+
+    def __init__(self, device=0):
+        self._p = lib().bg_aligner_new(int(device))
+        if not self._p:
+            raise NativeUnavailable("bg_aligner_new(%d) failed: no usable HIP device" % device)
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().bg_aligner_free(self._p)
+            self._p = None
+
+    __del__ = close
+
+    def set_tuning(self, R=0, waves=0):
+        check(lib().bg_set_tuning(self._p, R, waves))
+
+    @staticmethod
+    def _arrays(pairs):
+        n = len(pairs)
+        s1 = [bytes(p[0]) for p in pairs]
+        s2 = [bytes(p[1]) for p in pairs]
+        a1 = (ctypes.c_char_p * n)(*s1)
+        a2 = (ctypes.c_char_p * n)(*s2)
+        n1 = (ctypes.c_size_t * n)(*[len(x) for x in s1])
+        n2 = (ctypes.c_size_t * n)(*[len(x) for x in s2])
+        return a1, n1, a2, n2, sum(len(x) for x in s1) + sum(len(x) for x in s2)
+
+    def prepare(self, mode, pairs, scoring, a, b):
+        a1, n1, a2, n2, total = self._arrays(pairs)
+        self._keep = (a1, n1, a2, n2)
+        self._npairs = len(pairs)
+        self._total = total
+        check(lib().bg_batch_prepare(self._p, MODES.get(mode, mode), len(pairs), a1, n1, a2, n2,
+                                     ctypes.byref(scoring), a, b))
+
+    def execute(self):
+        check(lib().bg_batch_execute(self._p))
+
+    def synchronize(self):
+        check(lib().bg_synchronize(self._p))
+
+    def fetch(self):
+        n = self._npairs
+        res = (BgPairResult * max(n, 1))()
+        o1 = (ctypes.c_uint8 * max(self._total, 1))()
+        o2 = (ctypes.c_uint8 * max(self._total, 1))()
+        check(lib().bg_batch_fetch(self._p, res, o1, o2, self._total))
+        b1 = bytes(o1)
+        b2 = bytes(o2)
+        out = []
+        for p in range(n):
+            r = res[p]
+            lo, hi = r.offset, r.offset + r.len
+            out.append({"status": r.status, "score": r.score, "aligned1": b1[lo:hi],
+                        "aligned2": b2[lo:hi], "end": (r.end_i, r.end_j),
+                        "start": (r.start1, r.start2)})
+        return out
+
+    def align_batch(self, mode, pairs, scoring, a, b):
+        self.prepare(mode, pairs, scoring, a, b)
+        self.execute()
+        return self.fetch()
+
+    def stats(self):
+        st = BgStats()
+        check(lib().bg_get_stats(self._p, ctypes.byref(st)))
+        return {f: getattr(st, f) for f, _ in BgStats._fields_}

@@ -1,0 +1,73 @@
+// Shared host/device layout for the MI355X aligner (gfx950).
+//
+// One "batch" = many independent pairs (seq1 = rows, seq2 = columns) aligned with one mode,
+// one scoring table and one (open, extend) pair — exactly the arguments of one
+// SequenceAligner::*_alignment call in the reference (aligner.rs:84,150,216,290,351), applied to
+// a list of pairs.  Everything lives in HBM; see DESIGN.md "Data layout in HBM".
+#pragma once
+#include <stdint.h>
+
+#define BG_WAVE 64
+#define BG_CHUNK 64          // steps per chunk == columns per boundary block
+#define BG_TRACE_BLK 32      // steps per trace word (one bit per step per lane)
+
+// Modes, numbered like include/biogarden_gpu.h (bg_mode).
+enum { BGK_GLOBAL = 0, BGK_LOCAL = 1, BGK_FITTING = 2, BGK_OVERLAP = 3, BGK_SEMIGLOBAL = 4 };
+
+// Per-pair descriptor, built by the host planner (bg_host.cpp) in LPT order.
+struct BgPair {
+  uint64_t off1;       // byte offset of seq1 in the packed seq1 byte arena
+  uint64_t off2;       // byte offset of seq2 in the packed seq2 byte arena
+  uint64_t trace_off;  // byte offset of this pair's trace in the trace arena
+  uint64_t bnd_off;    // int32 offset of this pair's boundary rows (nstrips rows of NC*64)
+  uint64_t aux_off;    // int32 offset of this pair's aux area (lastcol n1+1 | rowbest n1 | rowpos n1)
+  uint64_t out_off;    // byte offset of this pair's output slot (capacity n1+n2)
+  int32_t n1, n2;
+  int32_t nstrips;     // ceil(n1 / (64 R)); 0 when n1 == 0 or n2 == 0 (no DP cells)
+  int32_t pad;         // virtual rows above row 1 in strip 0: nstrips*64R - n1
+  int32_t nc;          // chunks per strip: n2/64 + 2
+  int32_t index;       // caller's pair index (results are scattered back to it)
+};
+
+// Per-pair result written by the finish kernel.
+struct BgResult {
+  int32_t status;      // 0 ok, 4 reference would panic (traceback underflow)
+  int32_t score;
+  int32_t end_i, end_j;    // cell the traceback started from
+  uint32_t out_start;      // aligned strings occupy [out_start, n1+n2) of the pair's slot
+  uint32_t out_len;
+  uint32_t start1, start2; // cell (k, l) where the traceback walk stopped
+};
+
+struct BgDpArgs {
+  const BgPair* pairs;
+  const uint8_t* seq1;     // raw bytes of seq1, all pairs
+  const uint8_t* seq2;     // raw bytes of seq2, all pairs
+  const uint8_t* lut;      // 256 entries: byte -> dense code (DNA path: code*8)
+  uint32_t* trace;         // trace arena
+  int32_t* bndM;           // strip-boundary rows: M + open, per strip output
+  int32_t* bndX;           // strip-boundary rows: X (affine kernels only)
+  int32_t* aux;            // lastcol / rowbest / rowpos
+  const int32_t* profile;  // DNA: [k] int32 = 4 packed int8 S(q=k, c) - open; LDS path: int16 [32][32]
+  int32_t kdim;            // alphabet size (LDS path)
+  int32_t open, ext;       // reference `a`, `b`
+  int32_t mode;
+  int32_t npairs;
+};
+
+struct BgFinishArgs {
+  const BgPair* pairs;
+  const uint8_t* seq1;     // raw bytes (the aligned strings are built from them)
+  const uint8_t* seq2;
+  const uint32_t* trace;
+  const int32_t* bndM;
+  const int32_t* aux;
+  uint8_t* out1;           // aligned seq1, per-pair slot (written backwards)
+  uint8_t* out2;
+  BgResult* results;
+  int32_t open, ext;
+  int32_t mode;
+  int32_t R;               // rows per lane of the DP kernel that produced the trace
+  int32_t affine;          // trace carries x/y bits
+  int32_t npairs;
+};

@@ -1,0 +1,532 @@
+// Host runtime behind the C ABI (include/biogarden_gpu.h): validation in the reference's order,
+// batch planning (strips, LPT order, arenas in HBM), kernel launches on the handle's HIP
+// stream, download and unpacking of the aligned strings.
+//
+// Reference call sites mirrored here:
+//   argument checks      aligner.rs:87-89, 153-155, 219-225
+//   score closure        score.rs:38-41 (+ A.8 tabulation: bg_scoring)
+//   buffer semantics     aligner.rs:92-94, 594-602 (exact-size here; divergences are flagged)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <vector>
+
+#include "bg_device.h"
+#include "biogarden_gpu.h"
+
+extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
+extern "C" void* bg_finish_kernel_ptr();
+
+#include "bg_tables.inc"
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&p, want) != hipSuccess) { p = nullptr; return false; }
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+struct bg_aligner {
+  int device = 0;
+  int cus = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+  DevBuf seq1, seq2, lut, prof, pairs, trace, bndM, bndX, aux, out1, out2, results;
+
+  // prepared batch
+  bool prepared = false;
+  bool executed = false;
+  int mode = 0;
+  int32_t a = 0, b = 0;
+  size_t npairs = 0;
+  std::vector<size_t> n1v, n2v;
+  std::vector<int> prestatus;        // 1/2/3 = decided on the host; -1 = computed on the GPU
+  std::vector<uint64_t> outoff;      // caller output offsets
+  std::vector<BgPair> plan;          // GPU pairs in launch (LPT) order
+  std::vector<size_t> order_;        // plan slot -> caller index
+  int R = 8, W = 1, affine = 0, local = 0, dna = 1, kdim = 0;
+  size_t lds = 0;
+  uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
+  int tuneR = 0, tuneW = 0;
+  float dp_ms = 0.f, fin_ms = 0.f;
+
+  std::vector<BgResult> hres;
+  std::vector<uint8_t> ho1, ho2;
+
+  size_t device_bytes() const {
+    return seq1.cap + seq2.cap + lut.cap + prof.cap + pairs.cap + trace.cap + bndM.cap +
+           bndX.cap + aux.cap + out1.cap + out2.cap + results.cap;
+  }
+};
+
+static const char kDig[] = "0123456789ABCDEFGHIJKLMNOPQRSTUV";
+
+extern "C" int bg_scoring_builtin(int which, bg_scoring* out) {
+  if (!out) return BG_E_ARG;
+  const char* enc = which == BG_BLOSUM62 ? kBlosum62Enc : which == BG_PAM250 ? kPam250Enc
+                  : which == BG_UNIT ? kUnitEnc : nullptr;
+  if (!enc) return BG_E_ARG;
+  std::memset(out, 0, sizeof(*out));
+  out->alphabet_size = 26;
+  std::memset(out->code, 0xFF, sizeof(out->code));
+  for (int c = 0; c < 26; ++c) out->code['A' + c] = (uint8_t)c;  // score.rs:40 `(*a as usize) - 65`
+  for (int r = 0; r < 26; ++r)
+    for (int c = 0; c < 26; ++c) {
+      const char ch = enc[r * 26 + c];
+      const int v = (int)(std::strchr(kDig, ch) - kDig) - 8;
+      out->table[r * 32 + c] = v;
+    }
+  return BG_OK;
+}
+
+extern "C" const char* bg_status_string(int s) {
+  switch (s) {
+    case BG_OK: return "ok";
+    case BG_INVALID_ARGUMENT_RANGE: return "InvalidArgumentRange";
+    case BG_INVALID_INPUT_SIZE: return "InvalidInputSize";
+    case BG_UNSCORABLE: return "unscorable byte (reference panics)";
+    case BG_REF_DIVERGENT: return "reference would panic/hang (exact-size result returned)";
+    case BG_E_ARG: return "bad argument";
+    case BG_E_HIP: return "HIP error";
+    case BG_E_NOMEM: return "out of memory";
+    case BG_E_SCORE_RANGE: return "score - open does not fit int16";
+    case BG_E_NO_BATCH: return "no prepared batch";
+    case BG_E_ALPHABET: return "more than 32 symbols";
+    default: return "unknown";
+  }
+}
+
+extern "C" int bg_abi_version(void) { return BG_ABI_VERSION; }
+
+extern "C" bg_aligner* bg_aligner_new(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  bg_aligner* h = new bg_aligner();
+  h->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    h->cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return nullptr; }
+  for (auto& e : h->ev)
+    if (hipEventCreate(&e) != hipSuccess) { bg_aligner_free(h); return nullptr; }
+  return h;
+}
+
+extern "C" void bg_aligner_free(bg_aligner* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (DevBuf* d : {&h->seq1, &h->seq2, &h->lut, &h->prof, &h->pairs, &h->trace, &h->bndM, &h->bndX,
+                    &h->aux, &h->out1, &h->out2, &h->results})
+    d->release();
+  for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+extern "C" int bg_set_tuning(bg_aligner* h, int R, int waves) {
+  if (!h || (R != 0 && R != 4 && R != 8) || waves < 0 || waves > 16) return BG_E_ARG;
+  h->tuneR = R;
+  h->tuneW = waves;
+  return BG_OK;
+}
+
+#define BG_HIP(x)                          \
+  do {                                     \
+    if ((x) != hipSuccess) return BG_E_HIP; \
+  } while (0)
+
+extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
+                                const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                                const bg_scoring* sc, int32_t a, int32_t b) {
+  if (!h || !sc || mode < BG_GLOBAL || mode > BG_SEMIGLOBAL) return BG_E_ARG;
+  if (npairs && (!s1 || !n1 || !s2 || !n2)) return BG_E_ARG;
+  if (sc->alphabet_size < 0 || sc->alphabet_size > 32) return BG_E_ARG;
+  BG_HIP(hipSetDevice(h->device));
+  h->prepared = false;
+  h->executed = false;
+  h->mode = mode;
+  h->a = a;
+  h->b = b;
+  h->npairs = npairs;
+  h->n1v.assign(n1, n1 + npairs);
+  h->n2v.assign(n2, n2 + npairs);
+  h->prestatus.assign(npairs, -1);
+  h->outoff.resize(npairs);
+  uint64_t off = 0;
+  for (size_t p = 0; p < npairs; ++p) {
+    h->outoff[p] = off;
+    off += n1[p] + n2[p];
+  }
+  h->outBytes = off;
+
+  // ---- per-pair validation, in the reference's order
+  const bool needNonPos = mode == BG_GLOBAL || mode == BG_LOCAL || mode == BG_FITTING;
+  bool present[32] = {false};
+  for (size_t p = 0; p < npairs; ++p) {
+    if ((n1[p] && !s1[p]) || (n2[p] && !s2[p])) return BG_E_ARG;
+    if (n1[p] > 0x3FFFFFFF || n2[p] > 0x3FFFFFFF) return BG_E_ARG;
+    if (needNonPos && (a > 0 || b > 0)) { h->prestatus[p] = BG_INVALID_ARGUMENT_RANGE; continue; }
+    if (mode == BG_FITTING && n1[p] < n2[p]) { h->prestatus[p] = BG_INVALID_INPUT_SIZE; continue; }
+    if (n1[p] == 0 || n2[p] == 0) continue;           // the score closure is never called
+    bool bad = false;
+    bool loc[32] = {false};
+    for (size_t i = 0; i < n1[p] && !bad; ++i) {
+      const uint8_t c = sc->code[s1[p][i]];
+      if (c == 0xFF || c >= 32) bad = true; else loc[c] = true;
+    }
+    for (size_t j = 0; j < n2[p] && !bad; ++j) {
+      const uint8_t c = sc->code[s2[p][j]];
+      if (c == 0xFF || c >= 32) bad = true; else loc[c] = true;
+    }
+    if (bad) { h->prestatus[p] = BG_UNSCORABLE; continue; }
+    for (int c = 0; c < 32; ++c) present[c] |= loc[c];
+  }
+
+  // ---- dense alphabet, profile, kernel family
+  int dense[32];
+  int K = 0;
+  for (int c = 0; c < 32; ++c) dense[c] = present[c] ? K++ : -1;
+  int32_t maxAbsS = 0;
+  for (int q = 0; q < 32; ++q)
+    for (int c = 0; c < 32; ++c)
+      if (present[q] && present[c]) maxAbsS = std::max<int32_t>(maxAbsS, std::abs(sc->table[q * 32 + c]));
+  bool dnaOK = K <= 4;
+  bool i16OK = true;
+  for (int q = 0; q < 32; ++q)
+    for (int c = 0; c < 32; ++c) {
+      if (!present[q] || !present[c]) continue;
+      const int64_t v = (int64_t)sc->table[q * 32 + c] - (int64_t)a;
+      if (v < -128 || v > 127) dnaOK = false;
+      if (v < -32768 || v > 32767) i16OK = false;
+    }
+  if (!dnaOK && !i16OK) return BG_E_SCORE_RANGE;
+  h->dna = dnaOK ? 1 : 0;
+  h->kdim = std::max(K, 1);
+  h->local = mode == BG_LOCAL;
+
+  size_t maxn1 = 0, maxn2 = 0, ncomp = 0;
+  for (size_t p = 0; p < npairs; ++p)
+    if (h->prestatus[p] < 0) {
+      maxn1 = std::max(maxn1, n1[p]);
+      maxn2 = std::max(maxn2, n2[p]);
+      ++ncomp;
+    }
+  // linear-gap kernel iff a >= b (x/y traces provably 'M') and no intermediate can wrap
+  const double bound = ((double)maxAbsS + std::abs((double)a) + std::abs((double)b)) *
+                       ((double)maxn1 + (double)maxn2 + 2.0);
+  h->affine = (a >= b && bound < 1073741824.0) ? 0 : 1;
+
+  // ---- geometry: rows per lane, waves per workgroup
+  int R = h->tuneR ? h->tuneR : (maxn1 <= 256 ? 4 : 8);
+  int W = h->tuneW;
+  if (!W) {
+    const size_t maxStrips = maxn1 ? (maxn1 + 64 * R - 1) / (64 * R) : 1;
+    if (ncomp >= (size_t)4 * h->cus) W = 1;
+    else {
+      const size_t want = ((size_t)16 * h->cus + std::max<size_t>(ncomp, 1) - 1) / std::max<size_t>(ncomp, 1);
+      W = (int)std::min<size_t>({16, maxStrips, want});
+      W = std::max(W, 1);
+    }
+  }
+  if ((h->affine || h->local) && W > 8) W = 8;  // those kernels are built for <= 512 threads
+  size_t lds = 256;
+  if (!h->dna) {
+    const int WPE = (R + 1) / 2;
+    for (;;) {
+      lds = 256 + 2048 + (size_t)W * h->kdim * 64 * WPE * 4;
+      if (lds <= 160 * 1024 || W == 1) break;
+      --W;
+    }
+  }
+  h->R = R;
+  h->W = W;
+  h->lds = lds;
+
+  // ---- plan: LPT order, arenas
+  const int NW = h->affine ? 4 : 2;
+  std::vector<size_t> order;
+  for (size_t p = 0; p < npairs; ++p)
+    if (h->prestatus[p] < 0) order.push_back(p);
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+    return (uint64_t)n1[x] * n2[x] > (uint64_t)n1[y] * n2[y];
+  });
+  h->plan.clear();
+  h->plan.reserve(order.size());
+  uint64_t o1 = 0, o2 = 0, tro = 0, bo = 0, ao = 0, oo = 0;
+  h->cells = 0;
+  for (size_t p : order) {
+    BgPair P;
+    std::memset(&P, 0, sizeof(P));
+    P.n1 = (int32_t)n1[p];
+    P.n2 = (int32_t)n2[p];
+    P.index = (int32_t)h->plan.size();
+    P.off1 = o1; o1 += n1[p];
+    P.off2 = o2; o2 += n2[p];
+    const bool dp = n1[p] > 0 && n2[p] > 0;
+    P.nstrips = dp ? (int32_t)((n1[p] + 64 * R - 1) / (64 * R)) : 0;
+    P.pad = P.nstrips * 64 * R - P.n1;
+    P.nc = (int32_t)(n2[p] / 64 + 2);
+    P.trace_off = tro;
+    tro += round_up((uint64_t)P.nstrips * P.nc * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE * 4, 256);
+    P.bnd_off = bo;
+    bo += (uint64_t)P.nstrips * P.nc * BG_CHUNK;
+    P.aux_off = ao;
+    ao += round_up((uint64_t)(n1[p] + 1) + (h->local ? 2 * n1[p] : 0), 64);
+    P.out_off = oo;
+    oo += n1[p] + n2[p];
+    h->cells += (uint64_t)n1[p] * n2[p];
+    h->plan.push_back(P);
+  }
+  h->traceBytes = tro;
+  h->bndBytes = bo * 4 * (h->affine ? 2 : 1);
+  h->resBytes = o1 + o2;
+
+  // ---- device memory
+  if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->lut.ensure(256) ||
+      !h->prof.ensure(2048) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
+      !h->trace.ensure(tro + 256) || !h->bndM.ensure(bo * 4 + 256) ||
+      !h->bndX.ensure(h->affine ? bo * 4 + 256 : 256) || !h->aux.ensure(ao * 4 + 256) ||
+      !h->out1.ensure(oo + 16) || !h->out2.ensure(oo + 16) ||
+      !h->results.ensure(sizeof(BgResult) * (h->plan.size() + 1)))
+    return BG_E_NOMEM;
+
+  // ---- uploads
+  std::vector<uint8_t> st1(o1 + 1), st2(o2 + 1);
+  for (size_t q = 0; q < order.size(); ++q) {
+    const size_t p = order[q];
+    if (n1[p]) std::memcpy(st1.data() + h->plan[q].off1, s1[p], n1[p]);
+    if (n2[p]) std::memcpy(st2.data() + h->plan[q].off2, s2[p], n2[p]);
+  }
+  uint8_t lut[256];
+  for (int x = 0; x < 256; ++x) {
+    const uint8_t c = sc->code[x];
+    const int d = (c < 32 && dense[c] >= 0) ? dense[c] : 0;
+    lut[x] = (uint8_t)(h->dna ? d * 8 : d);
+  }
+  std::vector<int32_t> prof(512, 0);
+  if (h->dna) {
+    for (int q = 0; q < 32; ++q) {
+      if (dense[q] < 0) continue;
+      uint32_t packed = 0;
+      for (int c = 0; c < 32; ++c) {
+        if (dense[c] < 0) continue;
+        const int v = sc->table[q * 32 + c] - a;
+        packed |= (uint32_t)(uint8_t)(int8_t)v << (8 * dense[c]);
+      }
+      prof[dense[q]] = (int32_t)packed;
+    }
+  } else {
+    int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
+    for (int q = 0; q < 32; ++q)
+      for (int c = 0; c < 32; ++c)
+        if (dense[q] >= 0 && dense[c] >= 0) t16[dense[q] * 32 + dense[c]] = (int16_t)(sc->table[q * 32 + c] - a);
+  }
+  BG_HIP(hipMemcpyAsync(h->seq1.p, st1.data(), o1 + 1, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->seq2.p, st2.data(), o2 + 1, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->lut.p, lut, 256, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), 2048, hipMemcpyHostToDevice, h->stream));
+  if (!h->plan.empty())
+    BG_HIP(hipMemcpyAsync(h->pairs.p, h->plan.data(), sizeof(BgPair) * h->plan.size(),
+                          hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipStreamSynchronize(h->stream));
+  h->order_ = order;
+  h->prepared = true;
+  return BG_OK;
+}
+
+extern "C" int bg_batch_execute(bg_aligner* h) {
+  if (!h) return BG_E_ARG;
+  if (!h->prepared) return BG_E_NO_BATCH;
+  BG_HIP(hipSetDevice(h->device));
+  const unsigned np = (unsigned)h->plan.size();
+  BG_HIP(hipEventRecord(h->ev[0], h->stream));
+  if (np) {
+    void* fn = bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
+    if (!fn) return BG_E_ARG;
+    BgDpArgs A;
+    A.pairs = h->pairs.as<BgPair>();
+    A.seq1 = h->seq1.as<uint8_t>();
+    A.seq2 = h->seq2.as<uint8_t>();
+    A.lut = h->lut.as<uint8_t>();
+    A.trace = h->trace.as<uint32_t>();
+    A.bndM = h->bndM.as<int32_t>();
+    A.bndX = h->bndX.as<int32_t>();
+    A.aux = h->aux.as<int32_t>();
+    A.profile = h->prof.as<int32_t>();
+    A.kdim = h->kdim;
+    A.open = h->a;
+    A.ext = h->b;
+    A.mode = h->mode;
+    A.npairs = (int32_t)np;
+    void* args[] = {&A};
+    BG_HIP(hipLaunchKernel(fn, dim3(np), dim3(64 * h->W), args, h->lds, h->stream));
+  }
+  BG_HIP(hipEventRecord(h->ev[1], h->stream));
+  if (np) {
+    BgFinishArgs F;
+    F.pairs = h->pairs.as<BgPair>();
+    F.seq1 = h->seq1.as<uint8_t>();
+    F.seq2 = h->seq2.as<uint8_t>();
+    F.trace = h->trace.as<uint32_t>();
+    F.bndM = h->bndM.as<int32_t>();
+    F.aux = h->aux.as<int32_t>();
+    F.out1 = h->out1.as<uint8_t>();
+    F.out2 = h->out2.as<uint8_t>();
+    F.results = h->results.as<BgResult>();
+    F.open = h->a;
+    F.ext = h->b;
+    F.mode = h->mode;
+    F.R = h->R;
+    F.affine = h->affine;
+    F.npairs = (int32_t)np;
+    void* args[] = {&F};
+    BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(), dim3(np), dim3(64), args, 0, h->stream));
+  }
+  BG_HIP(hipEventRecord(h->ev[2], h->stream));
+  h->executed = true;
+  return BG_OK;
+}
+
+extern "C" int bg_synchronize(bg_aligner* h) {
+  if (!h) return BG_E_ARG;
+  BG_HIP(hipSetDevice(h->device));
+  BG_HIP(hipStreamSynchronize(h->stream));
+  if (h->executed) {
+    (void)hipEventElapsedTime(&h->dp_ms, h->ev[0], h->ev[1]);
+    (void)hipEventElapsedTime(&h->fin_ms, h->ev[1], h->ev[2]);
+  }
+  return BG_OK;
+}
+
+// Would a freshly constructed reference SequenceAligner (1024x1024 scratch, aligner.rs:44-55)
+// panic, hang or answer differently on this pair?  Exact-size semantics differ from it only when
+// it does not resize (both lengths <= 1024) and either indexes row/column 1024 or its end-cell
+// fold reaches stale cells beyond the pair's region (DESIGN.md "Buffer semantics").
+static bool ref_fresh_divergent(int mode, size_t n1, size_t n2, int32_t score) {
+  if (n1 > 1024 || n2 > 1024) return false;  // resized to exactly (n1+1, n2+1)
+  const bool edge1 = n1 == 1024, edge2 = n2 == 1024;
+  switch (mode) {
+    case BG_GLOBAL: return edge1 || edge2;
+    case BG_LOCAL: return (edge1 || edge2) && n1 > 0 && n2 > 0;
+    case BG_FITTING: return edge2 || (edge1 && n2 > 0) || (score < 0 && n1 + 1 < 1024);
+    case BG_OVERLAP: return edge1 || edge2 || (score <= 0 && n2 + 1 < 1024);
+    default: return edge1 || edge2 || (score == 0 && n2 + 1 < 1024);
+  }
+}
+
+extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1, uint8_t* out2,
+                              size_t out_cap) {
+  if (!h || (h->npairs && !res)) return BG_E_ARG;
+  if (!h->prepared || !h->executed) return BG_E_NO_BATCH;
+  if (h->outBytes && (!out1 || !out2 || out_cap < h->outBytes)) return BG_E_ARG;
+  int rc = bg_synchronize(h);
+  if (rc) return rc;
+  const size_t np = h->plan.size();
+  h->hres.resize(np);
+  uint64_t ob = 0;
+  for (const BgPair& P : h->plan) ob += (uint64_t)P.n1 + P.n2;
+  h->ho1.resize(ob + 1);
+  h->ho2.resize(ob + 1);
+  if (np) {
+    BG_HIP(hipMemcpyAsync(h->hres.data(), h->results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, h->stream));
+    BG_HIP(hipMemcpyAsync(h->ho1.data(), h->out1.p, ob, hipMemcpyDeviceToHost, h->stream));
+    BG_HIP(hipMemcpyAsync(h->ho2.data(), h->out2.p, ob, hipMemcpyDeviceToHost, h->stream));
+    BG_HIP(hipStreamSynchronize(h->stream));
+  }
+  for (size_t p = 0; p < h->npairs; ++p) {
+    std::memset(&res[p], 0, sizeof(res[p]));
+    res[p].status = h->prestatus[p] < 0 ? 0 : h->prestatus[p];
+    res[p].offset = h->outoff[p];
+  }
+  for (size_t q = 0; q < np; ++q) {
+    const BgPair& P = h->plan[q];
+    const BgResult& r = h->hres[q];
+    const size_t p = h->order_[q];
+    bg_pair_result& o = res[p];
+    o.status = r.status;
+    o.score = r.score;
+    o.len = r.out_len;
+    o.end_i = (uint32_t)r.end_i;
+    o.end_j = (uint32_t)r.end_j;
+    o.start1 = r.start1;
+    o.start2 = r.start2;
+    if (r.out_len > (uint32_t)(P.n1 + P.n2) || r.out_start + r.out_len > (uint32_t)(P.n1 + P.n2)) return BG_E_HIP;
+    std::memcpy(out1 + h->outoff[p], h->ho1.data() + P.out_off + r.out_start, r.out_len);
+    std::memcpy(out2 + h->outoff[p], h->ho2.data() + P.out_off + r.out_start, r.out_len);
+    if (o.status == BG_OK && ref_fresh_divergent(h->mode, h->n1v[p], h->n2v[p], r.score))
+      o.status = BG_REF_DIVERGENT;
+  }
+  return BG_OK;
+}
+
+extern "C" int bg_align_batch(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
+                              const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                              const bg_scoring* sc, int32_t a, int32_t b, bg_pair_result* res,
+                              uint8_t* out1, uint8_t* out2, size_t out_cap) {
+  int rc = bg_batch_prepare(h, mode, npairs, s1, n1, s2, n2, sc, a, b);
+  if (rc) return rc;
+  rc = bg_batch_execute(h);
+  if (rc) return rc;
+  return bg_batch_fetch(h, res, out1, out2, out_cap);
+}
+
+extern "C" int bg_align(bg_aligner* h, int mode, const uint8_t* s1, size_t n1, const uint8_t* s2,
+                        size_t n2, const bg_scoring* sc, int32_t a, int32_t b, int32_t* score,
+                        uint8_t* out1, uint8_t* out2, size_t cap, size_t* out_len) {
+  if (!h || !score || !out_len || cap < n1 + n2 || ((n1 + n2) && (!out1 || !out2))) return BG_E_ARG;
+  bg_pair_result r;
+  const uint8_t* p1 = s1;
+  const uint8_t* p2 = s2;
+  int rc = bg_align_batch(h, mode, 1, &p1, &n1, &p2, &n2, sc, a, b, &r, out1, out2, cap);
+  if (rc) return rc;
+  *score = r.score;
+  *out_len = r.len;
+  return r.status;
+}
+
+extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
+  if (!h || !o) return BG_E_ARG;
+  std::memset(o, 0, sizeof(*o));
+  o->cells = h->cells;
+  o->trace_bytes = h->traceBytes;
+  o->boundary_bytes = h->bndBytes;
+  o->residue_bytes = h->resBytes;
+  o->device_bytes = h->device_bytes();
+  o->R = h->R;
+  o->waves = h->W;
+  o->affine = h->affine;
+  o->dna = h->dna;
+  o->local = h->local;
+  o->npairs = (int32_t)h->npairs;
+  o->dp_ms = h->dp_ms;
+  o->finish_ms = h->fin_ms;
+  return BG_OK;
+}

@@ -1,0 +1,633 @@
+// MI355X (gfx950) kernels for the affine-gap pairwise aligner.
+//
+// Replaces the hot loops of the reference aligner (robsndr/biogarden):
+//   compute_scores_global  src/alignment/aligner.rs:437-469
+//   compute_scores_local   src/alignment/aligner.rs:471-509
+//   end-cell selection     aligner.rs:112,173-176,247-251,308-312,369-404
+//   backtrack              aligner.rs:511-592 (incl. the one-cell-late X/Y quirk)
+//
+// Geometry (DESIGN.md "Kernels"):
+//   * one workgroup per pair, W waves; a pair's rows are cut into strips of 64*R rows,
+//     strip s is owned by wave s % W.  Inside a strip, lane r owns rows [r*R, r*R+R) and the
+//     wave sweeps anti-diagonally: at step t lane r computes column j = t - r, so the row above
+//     (lane r-1's last row) arrives by one DPP wave_shr:1 per step and everything else stays in
+//     VGPRs.  No LDS traffic for scores at all on the DNA path.
+//   * strips are pipelined across the waves in phases of 64 steps separated by s_barrier;
+//     strip s runs chunk c in phase start(s)+c with start(s) >= start(s-1)+2, so the boundary
+//     row block a strip consumes was stored one phase earlier by the strip above.
+//   * the trace (2 bits/cell, +2 for the affine kernel) is built with v_cmp -> SGPR masks ->
+//     v_addc_co_u32 shift-in into per-lane 32-step words and streamed to HBM as coalesced
+//     256-B stores.  Scores never touch HBM except the strip-boundary rows.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bg_device.h"
+
+typedef unsigned long long u64;
+
+extern "C" __device__ int bg_writelane_i32(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+namespace {
+
+constexpr int kNegInf = INT32_MIN;  // i32::MIN: x/y buffers' initial value (aligner.rs:49-50)
+
+__device__ __forceinline__ int dpp_shr1(int old, int src) {
+  // v_mov_b32_dpp wave_shr:1 — lane r receives lane r-1; lane 0 keeps `old`.
+  return __builtin_amdgcn_update_dpp(old, src, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ int wrlane(int val, int l, int old) { return bg_writelane_i32(val, l, old); }
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+// release-mode i32 `+` wraps; `saturating_add` is v_add_i32 ... clamp
+__device__ __forceinline__ int wadd(int x, int y) { return (int)((unsigned)x + (unsigned)y); }
+__device__ __forceinline__ int wmul(int x, int y) { return (int)((unsigned)x * (unsigned)y); }
+__device__ __forceinline__ int sadd(int x, int y) { return __builtin_elementwise_add_sat(x, y); }
+__device__ __forceinline__ int imax(int x, int y) { return __builtin_elementwise_max(x, y); }
+// v_max3_i32 kept opaque so the compiler cannot turn `best == y` into a max+compare pair.
+__device__ __forceinline__ int imax3(int x, int y, int z) {
+  int r;
+  asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+  return r;
+}
+__device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
+__device__ __forceinline__ int sbfe(int v, int off, int w) { return __builtin_amdgcn_sbfe(v, off, w); }
+
+// acc = 2*acc + (this lane's bit of mask): one VALU op per trace bit.
+__device__ __forceinline__ unsigned shift_in(unsigned acc, u64 mask) {
+  unsigned r;
+  u64 co;
+  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(acc), "s"(mask));
+  return r;
+}
+
+// v_cndmask_b32 kept opaque: a plain `gt ? best : old` chain over the unrolled steps is
+// re-associated by LLVM into a max-tree that keeps every step's value live (register spills).
+__device__ __forceinline__ int vsel(u64 mask, int if_set, int if_clear) {
+  int r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(mask));
+  return r;
+}
+
+__device__ __forceinline__ int load_agent(const int32_t* p) {
+  // L1-bypassing load (global_load_dword sc1): boundary rows written by another wave.
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Row 0 / column 0 initialisation per mode (aligner.rs:96-104, 163, 233-237, 299, 360).
+__device__ __forceinline__ int row0_M(int mode, int j, int a, int b) {
+  if (j == 0) return 0;
+  return (mode == BGK_GLOBAL || mode == BGK_FITTING) ? wadd(a, wmul(j - 1, b)) : 0;
+}
+__device__ __forceinline__ int col0_M(int mode, int i, int a, int b) {
+  if (i == 0) return 0;
+  return (mode == BGK_GLOBAL) ? wadd(a, wmul(i - 1, b)) : 0;
+}
+
+template <int R, bool AFFINE, bool LOCAL>
+struct Strip {
+  int Ma[R];               // M(i_k, j-1) + a   (the "left" of the next step)
+  int Y[AFFINE ? R : 1];   // Y(i_k, j-1)
+  unsigned tA[R];          // trace word: m-trace bit 0  ('Y', or STOP in local mode)
+  unsigned tB[R];          // trace word: m-trace bit 1  ('X' and not 'Y', or STOP)
+  unsigned tC[AFFINE ? R : 1];  // x_trace == 'M'
+  unsigned tD[AFFINE ? R : 1];  // y_trace == 'M'
+  int bestv[LOCAL ? R : 1];     // local: running row maximum
+  int bpos[LOCAL ? R : 1];      // local: step of the first maximum
+  int prof[R];             // DNA path: 4 packed int8 S(q, c) - a
+  int topPrev;             // M(row above, j-1) + a  for row 0 of the lane
+  int Xlast;               // X of the lane's last row (fed to the lane below)
+  int code;                // target residue code of this lane's current column
+  int oM, oX;              // boundary-row output accumulators (one 64-column block)
+};
+
+struct Ctx {
+  int a, b, mode;
+  int n1, n2, nc, nst, s;
+  int rowbase;             // first 0-based row of this lane: s*64R + lane*R
+  int olane, orow;         // which lane / row feeds the boundary output (last strip: row n1)
+  uint32_t* trace;         // this strip's trace base
+  int32_t* bndOutM;        // this strip's output row (M + a)
+  int32_t* bndOutX;
+  int32_t* lastcol;        // M(i, n2), i = 0..n1
+  const int* ldsProf;      // LDS path: this wave's per-lane table
+  int lane;
+};
+
+template <int R, bool AFFINE, bool LOCAL, bool DNA, bool SLOW>
+__device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx& C, int c, int bM,
+                                          int bX, int cv) {
+  const int a = C.a;
+  const int b = C.b;
+  const int lane = C.lane;
+  const int t0 = c * BG_CHUNK;
+  constexpr int NW = AFFINE ? 4 : 2;
+#pragma unroll 1
+  for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h) {
+#pragma unroll
+  for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
+    const int u = h * BG_TRACE_BLK + uu;
+    const int t = t0 + u;
+    // ---- inputs from the row above: lane r-1's last row at this column, or the boundary row
+    const int topMa = dpp_shr1(rdlane(bM, u), S.Ma[R - 1]);
+    int topX = 0;
+    if constexpr (AFFINE) topX = dpp_shr1(rdlane(bX, u), S.Xlast);
+    S.code = dpp_shr1(rdlane(cv, u), S.code);
+    int lp[DNA ? 1 : (R + 1) / 2];
+    if constexpr (!DNA) {
+      if constexpr (R == 8) {
+        const int4 v = *reinterpret_cast<const int4*>(C.ldsProf + (S.code * BG_WAVE + lane) * 4);
+        lp[0] = v.x; lp[1] = v.y; lp[2] = v.z; lp[3] = v.w;
+      } else if constexpr (R == 4) {
+        const int2 v = *reinterpret_cast<const int2*>(C.ldsProf + (S.code * BG_WAVE + lane) * 2);
+        lp[0] = v.x; lp[1] = v.y;
+      } else {
+#pragma unroll
+        for (int q = 0; q < (R + 1) / 2; ++q) lp[q] = C.ldsProf[(S.code * BG_WAVE + lane) * ((R + 1) / 2) + q];
+      }
+    }
+    bool valid = true;
+    if constexpr (SLOW && LOCAL) valid = (t - lane >= 1) && (t - lane <= C.n2);
+    int diag = S.topPrev;
+    int xo = topMa;
+    int xt = topX;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      int sp;
+      if constexpr (DNA) sp = sbfe(S.prof[k], S.code, 8);
+      else sp = sbfe(lp[k >> 1], (k & 1) * 16, 16);
+      const int d = wadd(diag, sp);           // M(i-1,j-1) + S(seq1[i-1], seq2[j-1])
+      const int yo = S.Ma[k];                 // M(i,j-1) + a
+      int X, Yv;
+      u64 mXt = 0, mYt = 0;
+      if constexpr (AFFINE) {
+        const int xs = sadd(xt, b);           // X(i-1,j).saturating_add(b)
+        const int ys = sadd(S.Y[k], b);       // Y(i,j-1).saturating_add(b)
+        mXt = ballot(xo >= xs);               // x_trace == 'M'  (aligner.rs:444/478)
+        mYt = ballot(yo >= ys);               // y_trace == 'M'  (:448/484)
+        if constexpr (LOCAL) { X = imax3(xo, xs, 0); Yv = imax3(yo, ys, 0); }  // clamp after trace
+        else { X = imax(xo, xs); Yv = imax(yo, ys); }
+        S.Y[k] = Yv;
+      } else {
+        // a >= b: X == M(i-1,j)+a and Y == M(i,j-1)+a exactly, x/y_trace == 'M' 
+        if constexpr (LOCAL) { X = imax(xo, 0); Yv = imax(yo, 0); }
+        else { X = xo; Yv = yo; }
+      }
+      const int best = imax3(d, X, Yv);
+      u64 mY = ballot(best == Yv);            // priority Y > X > R (aligner.rs:455-463)
+      u64 mX = ballot(best == X) & ~mY;
+      if constexpr (LOCAL) {
+        const u64 z = ballot(best == 0);      // M == 0: backtrack stops here (:181)
+        mY |= z;
+        mX |= z;
+        const u64 gt = ballot(valid && (best > S.bestv[k]));
+        S.bestv[k] = vsel(gt, best, S.bestv[k]);
+        S.bpos[k] = vsel(gt, t, S.bpos[k]);
+      }
+      S.tA[k] = shift_in(S.tA[k], mY);
+      S.tB[k] = shift_in(S.tB[k], mX);
+      if constexpr (AFFINE) {
+        S.tC[k] = shift_in(S.tC[k], mXt);
+        S.tD[k] = shift_in(S.tD[k], mYt);
+      }
+      const int man = wadd(best, a);          // local: best >= 0 already, so M = best
+      diag = yo;                              // M(i,j-1)+a = diagonal input of row i+1 (+S-a)
+      xo = man;                               // M(i,j)+a   = vertical input of row i+1
+      if constexpr (AFFINE) xt = X;
+      S.Ma[k] = man;
+    }
+    S.topPrev = topMa;
+    if constexpr (AFFINE) S.Xlast = xt;
+
+    if constexpr (SLOW) {
+      // column 0: this lane is at j == 0 -> load the border (aligner.rs:98-104 / fill(0))
+      if (c == 0) {
+        const bool rst = (t == lane);
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int i = C.rowbase + k + 1;
+          const int border = wadd(col0_M(C.mode, i, a, b), a);
+          S.Ma[k] = rst ? border : S.Ma[k];
+          if constexpr (AFFINE) S.Y[k] = rst ? kNegInf : S.Y[k];
+        }
+      }
+      // last column j == n2: M(i, n2) for the end-cell searches
+      if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {
+        if (lane == t - C.n2) {
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const int i = C.rowbase + k + 1;
+            if (i <= C.n1) C.lastcol[i] = wadd(S.Ma[k], -a);
+          }
+        }
+      }
+    }
+
+    // ---- boundary output: row `orow` of lane `olane` at column t - olane
+    {
+      int sel = S.Ma[R - 1];
+      if constexpr (SLOW) {
+#pragma unroll
+        for (int k = 0; k < R - 1; ++k) sel = (C.orow == k) ? S.Ma[k] : sel;
+      }
+      const int jo = t - C.olane;
+      if (!SLOW || (jo >= 0 && jo <= C.n2)) {
+        S.oM = wrlane(rdlane(sel, C.olane), jo & 63, S.oM);
+        if constexpr (AFFINE) S.oX = wrlane(rdlane(S.Xlast, C.olane), jo & 63, S.oX);
+        if ((jo & 63) == 63 || (SLOW && jo == C.n2)) {
+          const int blk = jo & ~63;
+          C.bndOutM[blk + lane] = S.oM;
+          if constexpr (AFFINE) C.bndOutX[blk + lane] = S.oX;
+        }
+      }
+    }
+
+  }
+  // ---- trace flush every 32 steps: R*NW coalesced 256-B stores
+  {
+    uint32_t* tb = C.trace + (size_t)((t0 >> 5) + h) * (R * NW * BG_WAVE) + lane;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      tb[(k * NW + 0) * BG_WAVE] = S.tA[k];
+      tb[(k * NW + 1) * BG_WAVE] = S.tB[k];
+      if constexpr (AFFINE) {
+        tb[(k * NW + 2) * BG_WAVE] = S.tC[k];
+        tb[(k * NW + 3) * BG_WAVE] = S.tD[k];
+      }
+    }
+  }
+  }
+}
+
+}  // namespace
+
+template <int R, bool AFFINE, bool LOCAL, bool DNA>
+__global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(BgDpArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* sLut = smem;                                        // 256 B
+  int16_t* sTab = reinterpret_cast<int16_t*>(smem + 256);      // 32x32 int16 (LDS path)
+  const int lane = threadIdx.x & 63;
+  const int W = blockDim.x >> 6;
+  const int w = uni(threadIdx.x >> 6);
+  constexpr int NW = AFFINE ? 4 : 2;
+  constexpr int ROWS = BG_WAVE * R;
+
+  for (int x = threadIdx.x; x < 256; x += blockDim.x) sLut[x] = A.lut[x];
+  if constexpr (!DNA) {
+    const int16_t* g = reinterpret_cast<const int16_t*>(A.profile);
+    for (int x = threadIdx.x; x < 1024; x += blockDim.x) sTab[x] = g[x];
+  }
+  __syncthreads();
+
+  const BgPair& P = A.pairs[blockIdx.x];
+  const int n1 = P.n1, n2 = P.n2, nst = P.nstrips, NC = P.nc;
+  if (nst == 0) return;
+  const uint8_t* s1 = A.seq1 + P.off1;
+  const uint8_t* s2 = A.seq2 + P.off2;
+  const int a = A.open;
+  const int b = A.ext;
+  const int mode = A.mode;
+  const size_t stripDw = (size_t)NC * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE;
+
+  int* ldsProf = nullptr;
+  if constexpr (!DNA) ldsProf = reinterpret_cast<int*>(smem + 256 + 2048) + (size_t)w * A.kdim * BG_WAVE * ((R + 1) / 2);
+
+  Ctx C;
+  C.a = a; C.b = b; C.mode = mode;
+  C.n1 = n1; C.n2 = n2; C.nc = NC; C.nst = nst;
+  C.lane = lane;
+  C.lastcol = A.aux + P.aux_off;
+  C.ldsProf = ldsProf;
+
+  Strip<R, AFFINE, LOCAL> S;
+  const int stride = NC > 2 * W ? NC : 2 * W;
+  const int lastS = nst - 1;
+  const int total = (lastS / W) * stride + 2 * (lastS % W) + NC;
+  int s = w;
+  int sstart = 2 * w;
+  int cvNext = 0;
+
+  for (int p = 0; p < total; ++p) {
+    if (s < nst && p >= sstart) {
+      const int c = p - sstart;
+      if (c == 0) {
+        // ---------------- strip begin
+        C.s = s;
+        C.rowbase = s * ROWS + lane * R;
+        const bool lastStrip = (s == nst - 1);
+        const int lastRow = n1 - 1 - s * ROWS;                 // row n1, 0-based within the strip
+        C.olane = lastStrip ? lastRow / R : BG_WAVE - 1;
+        C.orow = lastStrip ? lastRow % R : R - 1;
+        C.trace = A.trace + P.trace_off / 4 + (size_t)s * stripDw;
+        C.bndOutM = A.bndM + P.bnd_off + (size_t)s * NC * BG_CHUNK;
+        C.bndOutX = AFFINE ? A.bndX + P.bnd_off + (size_t)s * NC * BG_CHUNK : nullptr;
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int i = C.rowbase + k + 1;                       // 1-based row
+          const int q = (i <= n1) ? sLut[s1[i - 1]] : 0;
+          if constexpr (DNA) S.prof[k] = A.profile[q >> 3];
+          S.Ma[k] = wadd(col0_M(mode, i, a, b), a);
+          if constexpr (AFFINE) { S.Y[k] = kNegInf; S.tC[k] = 0; S.tD[k] = 0; }
+          S.tA[k] = 0; S.tB[k] = 0;
+          if constexpr (LOCAL) { S.bestv[k] = (i <= n1) ? INT32_MIN : INT32_MAX; S.bpos[k] = 0; }
+        }
+        if constexpr (!DNA) {
+          // per-lane table [code][lane] of R int16 S(q_k, code) - a, 2R bytes per entry
+          constexpr int WPE = (R + 1) / 2;
+          for (int cd = 0; cd < A.kdim; ++cd) {
+#pragma unroll
+            for (int q2 = 0; q2 < WPE; ++q2) {
+              int v = 0;
+#pragma unroll
+              for (int h = 0; h < 2; ++h) {
+                const int k = q2 * 2 + h;
+                if (k < R) {
+                  const int i = C.rowbase + k + 1;
+                  const int qq = (i <= n1) ? sLut[s1[i - 1]] : 0;
+                  v |= ((int)(uint16_t)sTab[qq * 32 + cd]) << (16 * h);
+                }
+              }
+              ldsProf[(cd * BG_WAVE + lane) * WPE + q2] = v;
+            }
+          }
+        }
+        S.topPrev = 0; S.Xlast = kNegInf; S.code = 0; S.oM = 0; S.oX = 0;
+        {
+          const int j = lane;                                   // codes of chunk 0
+          cvNext = (j >= 1 && j <= n2) ? sLut[s2[j - 1]] : 0;
+        }
+      }
+      // ---------------- chunk c: inputs
+      const int cv = cvNext;
+      {
+        const int j = (c + 1) * BG_CHUNK + lane;                 // prefetch codes of chunk c+1
+        cvNext = (j >= 1 && j <= n2) ? sLut[s2[j - 1]] : 0;
+      }
+      const int jb = c * BG_CHUNK + lane;
+      int bM, bX = kNegInf;
+      if (s == 0) {
+        bM = wadd(row0_M(mode, jb, a, b), a);
+      } else {
+        const int32_t* src = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb;
+        bM = load_agent(src);
+        if constexpr (AFFINE) bX = load_agent(A.bndX + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
+      }
+      const bool slow = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2) || (s == nst - 1);
+      if (slow) run_chunk<R, AFFINE, LOCAL, DNA, true>(S, C, c, bM, bX, cv);
+      else run_chunk<R, AFFINE, LOCAL, DNA, false>(S, C, c, bM, bX, cv);
+
+      if (c == NC - 1) {
+        // ---------------- strip end
+        if constexpr (LOCAL) {
+          int32_t* rowbest = A.aux + P.aux_off + (n1 + 1);
+          int32_t* rowpos = rowbest + n1;
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const int i = C.rowbase + k + 1;
+            if (i <= n1) { rowbest[i - 1] = S.bestv[k]; rowpos[i - 1] = S.bpos[k] - lane; }
+          }
+        }
+        s += W;
+        sstart += stride;
+      }
+    }
+    if (W > 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // boundary stores visible before the barrier
+      __syncthreads();
+    }
+  }
+}
+
+// ------------------------------------------------------------------ finish: end cell + traceback
+
+namespace {
+
+struct Fin {
+  const BgFinishArgs* F;
+  const BgPair* P;
+  int n1, n2, a, b, mode;
+  const uint8_t* s1;
+  const uint8_t* s2;
+  const int32_t* lastrowMa;   // bndM row of the last strip = M(n1, j) + a
+  const int32_t* lastcol;     // M(i, n2)
+};
+
+__device__ __forceinline__ int lastrowM(const Fin& f, int j) {
+  if (f.n1 == 0) return row0_M(f.mode, j, f.a, f.b);
+  if (j == 0) return col0_M(f.mode, f.n1, f.a, f.b);
+  return wadd(f.lastrowMa[j], -f.a);
+}
+__device__ __forceinline__ int lastcolM(const Fin& f, int i) {
+  if (f.n2 == 0) return col0_M(f.mode, i, f.a, f.b);
+  if (i == 0) return row0_M(f.mode, f.n2, f.a, f.b);
+  return f.lastcol[i];
+}
+
+// 64-bit key max over the wave
+__device__ __forceinline__ u64 wave_max_u64(u64 v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned lo = __shfl_xor((unsigned)v, o, 64);
+    const unsigned hi = __shfl_xor((unsigned)(v >> 32), o, 64);
+    const u64 other = ((u64)hi << 32) | lo;
+    v = other > v ? other : v;
+  }
+  return v;
+}
+__device__ __forceinline__ unsigned bias(int v) { return (unsigned)v ^ 0x80000000u; }
+__device__ __forceinline__ int unbias(unsigned v) { return (int)(v ^ 0x80000000u); }
+
+}  // namespace
+
+__global__ __launch_bounds__(64) void bg_finish_kernel(BgFinishArgs F) {
+  const BgPair& P = F.pairs[blockIdx.x];
+  const int lane = threadIdx.x;
+  Fin f;
+  f.F = &F; f.P = &P;
+  f.n1 = P.n1; f.n2 = P.n2; f.a = F.open; f.b = F.ext; f.mode = F.mode;
+  f.s1 = F.seq1 + P.off1;
+  f.s2 = F.seq2 + P.off2;
+  const int R = F.R;
+  const int NW = F.affine ? 4 : 2;
+  f.lastrowMa = (P.nstrips > 0) ? F.bndM + P.bnd_off + (size_t)(P.nstrips - 1) * P.nc * BG_CHUNK : nullptr;
+  f.lastcol = F.aux + P.aux_off;
+  const int n1 = f.n1, n2 = f.n2;
+
+  // ---------------- end cell (aligner.rs:112, 173-176, 247-251, 308-312, 369-389)
+  int ei = n1, ej = n2, score = 0, colcase = 0;
+  if (f.mode == BGK_GLOBAL) {
+    score = lastcolM(f, n1);
+  } else if (f.mode == BGK_LOCAL) {
+    // first row-major cell with the strict maximum; (0,0) with 0 when nothing is positive
+    u64 key = 0;
+    const int32_t* rowbest = f.lastcol + (n1 + 1);
+    const int32_t* rowpos = rowbest + n1;
+    if (n2 > 0)
+      for (int i = 1 + lane; i <= n1; i += 64) {
+        const u64 kk = ((u64)bias(rowbest[i - 1]) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+        key = kk > key ? kk : key;
+      }
+    key = wave_max_u64(key);
+    const int v = unbias((unsigned)(key >> 32));
+    if (key != 0 && v > 0) {
+      ei = (int)(0xFFFFFFFFu - (unsigned)key);
+      ej = rowpos[ei - 1];
+      score = v;
+    } else {
+      ei = 0; ej = 0; score = 0;
+    }
+  } else if (f.mode == BGK_FITTING) {
+    u64 key = 0;                                   // first i, strict > (:247-249)
+    for (int i = lane; i <= n1; i += 64) {
+      const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+      key = kk > key ? kk : key;
+    }
+    key = wave_max_u64(key);
+    ei = (int)(0xFFFFFFFFu - (unsigned)key); ej = n2; score = unbias((unsigned)(key >> 32));
+  } else if (f.mode == BGK_OVERLAP) {
+    u64 key = 0;                                   // last j, >= (:308-310)
+    for (int j = lane; j <= n2; j += 64) {
+      const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
+      key = kk > key ? kk : key;
+    }
+    key = wave_max_u64(key);
+    ei = n1; ej = (int)(unsigned)key; score = unbias((unsigned)(key >> 32));
+  } else {
+    u64 kr = 0, kc = 0;
+    for (int j = lane; j <= n2; j += 64) {         // last row, >= (:369-371)
+      const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
+      kr = kk > kr ? kk : kr;
+    }
+    for (int i = lane; i <= n1; i += 64) {         // last column, > (:376-378)
+      const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+      kc = kk > kc ? kk : kc;
+    }
+    kr = wave_max_u64(kr);
+    kc = wave_max_u64(kc);
+    const int mr = unbias((unsigned)(kr >> 32)), mc = unbias((unsigned)(kc >> 32));
+    colcase = mc > mr;                             // (:389)
+    if (colcase) { ei = (int)(0xFFFFFFFFu - (unsigned)kc); ej = n2; score = mc; }
+    else { ei = n1; ej = (int)(unsigned)kr; score = mr; }
+  }
+  if (lane != 0) return;
+
+  // ---------------- traceback (aligner.rs:511-592), written backwards into the pair's slot
+  uint8_t* o1 = F.out1 + P.out_off;
+  uint8_t* o2 = F.out2 + P.out_off;
+  int pos = n1 + n2;
+  int status = 0;
+  auto emit = [&](uint8_t c1, uint8_t c2) { --pos; o1[pos] = c1; o2[pos] = c2; };
+  int k = ei, l = ej;
+  if (f.mode == BGK_SEMIGLOBAL) {                  // tail gaps (:389-404)
+    if (colcase) for (int i = n1; i >= ei + 1; --i) emit(f.s1[i - 1], '-');
+    else for (int j = n2; j >= ej + 1; --j) emit('-', f.s2[j - 1]);
+  }
+  const uint32_t* tr = F.trace + P.trace_off / 4;
+  const int ROWS = 64 * R;
+  const size_t stripDw = (size_t)P.nc * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE;
+  // trace bits of interior cell (k,l): bit0 = m0, bit1 = m1, bit2 = x_trace=='M', bit3 = y_trace=='M'
+  auto fetch = [&](int kk, int ll) -> int {
+    const int vr = kk - 1;
+    const int sidx = vr / ROWS, rem = vr % ROWS, r = rem / R, q = rem % R;
+    const int t = ll + r;
+    const size_t base = (size_t)sidx * stripDw + ((size_t)(t >> 5) * R + q) * NW * BG_WAVE + r;
+    const int bit = 31 - (t & 31);
+    int v = ((tr[base] >> bit) & 1) | (((tr[base + BG_WAVE] >> bit) & 1) << 1);
+    if (F.affine) v |= (((tr[base + 2 * BG_WAVE] >> bit) & 1) << 2) | (((tr[base + 3 * BG_WAVE] >> bit) & 1) << 3);
+    else v |= 12;
+    return v;
+  };
+  int state = 0;  // 0 = M, 1 = X, 2 = Y
+  for (;;) {
+    // trace_valid (:117, :181, :256, :317, :409)
+    bool ok;
+    int bits = 0;
+    const bool interior = k > 0 && l > 0;
+    if (interior) bits = fetch(k, l);
+    if (f.mode == BGK_GLOBAL) ok = (k != 0 || l != 0);
+    else if (f.mode == BGK_LOCAL) ok = interior && (bits & 3) != 3;
+    else if (f.mode == BGK_SEMIGLOBAL) ok = interior;
+    else ok = l != 0;
+    if (!ok) break;
+    if (state == 0) {
+      // m_trace: borders column 0 = 'X', row 0 = 'Y' (row fill last, so (0,0) = 'Y')
+      int mt;  // 0 R, 1 X, 2 Y
+      if (!interior) mt = (k == 0) ? 2 : 1;
+      else mt = (bits & 1) ? 2 : ((bits & 2) ? 1 : 0);
+      if (mt == 0) {
+        if (k == 0 || l == 0) { status = 4; break; }
+        emit(f.s1[k - 1], f.s2[l - 1]); --k; --l;
+      } else if (mt == 1) {
+        state = 1;
+        if (k == 0) { status = 4; break; }
+        emit(f.s1[k - 1], '-'); --k;
+      } else {
+        state = 2;
+        if (l == 0) { status = 4; break; }
+        emit('-', f.s2[l - 1]); --l;
+      }
+    } else if (state == 1) {
+      const bool toM = interior && (bits & 4);      // x_trace border = 'I'
+      if (toM) state = 0;
+      else { if (k == 0) { status = 4; break; } emit(f.s1[k - 1], '-'); --k; }
+    } else {
+      const bool toM = interior && (bits & 8);
+      if (toM) state = 0;
+      else { if (l == 0) { status = 4; break; } emit('-', f.s2[l - 1]); --l; }
+    }
+  }
+  const int start1 = k, start2 = l;                  // where the walk stopped
+  if (status == 0 && f.mode == BGK_SEMIGLOBAL) {    // prefix gaps (:416-428)
+    if (colcase) for (int i = k; i >= 1; --i) emit(f.s1[i - 1], '-');
+    else for (int j = l; j >= 1; --j) emit('-', f.s2[j - 1]);
+  }
+  BgResult res;
+  res.status = status;
+  res.score = score;
+  res.end_i = ei;
+  res.end_j = ej;
+  res.out_start = (uint32_t)pos;
+  res.out_len = (uint32_t)(n1 + n2 - pos);
+  res.start1 = (uint32_t)start1;
+  res.start2 = (uint32_t)start2;
+  F.results[P.index] = res;
+}
+
+// ------------------------------------------------------------------ instantiation table
+
+typedef void (*bg_dp_fn)(BgDpArgs);
+
+#define BG_INST(R, AF, LO, DNA) \
+  template __global__ void bg_dp_kernel<R, AF, LO, DNA>(BgDpArgs);
+
+#define BG_INST_R(R)            \
+  BG_INST(R, false, false, true) \
+  BG_INST(R, false, true, true)  \
+  BG_INST(R, true, false, true)  \
+  BG_INST(R, true, true, true)   \
+  BG_INST(R, false, false, false) \
+  BG_INST(R, false, true, false)  \
+  BG_INST(R, true, false, false)  \
+  BG_INST(R, true, true, false)
+
+BG_INST_R(4)
+BG_INST_R(8)
+
+extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna) {
+#define BG_PICK(RR)                                                                        \
+  if (R == RR) {                                                                           \
+    if (!affine && !local && dna) return (void*)&bg_dp_kernel<RR, false, false, true>;     \
+    if (!affine && local && dna) return (void*)&bg_dp_kernel<RR, false, true, true>;       \
+    if (affine && !local && dna) return (void*)&bg_dp_kernel<RR, true, false, true>;       \
+    if (affine && local && dna) return (void*)&bg_dp_kernel<RR, true, true, true>;         \
+    if (!affine && !local && !dna) return (void*)&bg_dp_kernel<RR, false, false, false>;   \
+    if (!affine && local && !dna) return (void*)&bg_dp_kernel<RR, false, true, false>;     \
+    if (affine && !local && !dna) return (void*)&bg_dp_kernel<RR, true, false, false>;     \
+    if (affine && local && !dna) return (void*)&bg_dp_kernel<RR, true, true, false>;       \
+  }
+  BG_PICK(4)
+  BG_PICK(8)
+#undef BG_PICK
+  return nullptr;
+}
+
+extern "C" void* bg_finish_kernel_ptr() { return (void*)&bg_finish_kernel; }

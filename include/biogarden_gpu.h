@@ -1,0 +1,147 @@
+/*
+ * biogarden_gpu.h — C ABI of the MI355X-native aligner (libbiogarden_gpu.so).
+ *
+ * Drop-in boundary for robsndr/biogarden's alignment hot path.  Each entry point names the
+ * reference interface it replaces (paths relative to the reference crate root):
+ *
+ *   bg_aligner_new / bg_aligner_free   SequenceAligner::new / Default / drop
+ *                                      (src/alignment/aligner.rs:44-55, 605-609)
+ *   bg_align(mode=BG_GLOBAL)           SequenceAligner::global_alignment      (aligner.rs:84-121)
+ *   bg_align(mode=BG_LOCAL)            SequenceAligner::local_alignment       (aligner.rs:150-185)
+ *   bg_align(mode=BG_FITTING)          SequenceAligner::fitting_alignment     (aligner.rs:216-260)
+ *   bg_align(mode=BG_OVERLAP)          SequenceAligner::overlap_alignment     (aligner.rs:290-321)
+ *   bg_align(mode=BG_SEMIGLOBAL)       SequenceAligner::semiglobal_alignment  (aligner.rs:351-435)
+ *   bg_align_batch                     the same call over a Tile of pairs (ds/tile.rs:9-11)
+ *   bg_scoring_builtin                 score::blosum62 / pam250 / unit        (score.rs:38,78,114)
+ *   bg_scoring (struct)                the `&dyn Fn(&u8,&u8)->i32` closure, tabulated as data
+ *   status codes                       BioError::{InvalidArgumentRange, InvalidInputSize}
+ *                                      (error.rs:8-14) + the reference's panics
+ *
+ * Semantics: identical integer score and aligned strings to the reference for every input on
+ * which the reference returns (including its traceback quirks); see DESIGN.md.  Plain pointers
+ * and sizes only; no allocation crosses the boundary; one in-flight call per handle.
+ */
+#ifndef BIOGARDEN_GPU_H
+#define BIOGARDEN_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BG_ABI_VERSION 1
+
+typedef enum bg_mode {
+  BG_GLOBAL = 0,
+  BG_LOCAL = 1,
+  BG_FITTING = 2,
+  BG_OVERLAP = 3,
+  BG_SEMIGLOBAL = 4
+} bg_mode;
+
+/* Per-pair status (bg_pair_result.status, bg_align return value). */
+enum {
+  BG_OK = 0,
+  BG_INVALID_ARGUMENT_RANGE = 1, /* Err(BioError::InvalidArgumentRange): a > 0 || b > 0 (global/local/fitting) */
+  BG_INVALID_INPUT_SIZE = 2,     /* Err(BioError::InvalidInputSize): fitting with len1 < len2 */
+  BG_UNSCORABLE = 3,             /* the reference panics in the score closure (byte outside its table) */
+  BG_REF_DIVERGENT = 4           /* the reference (fresh SequenceAligner) panics or hangs on this input;
+                                    the result of the exactly-sized DP is returned and flagged */
+};
+
+/* Call-level errors (negative return values). */
+enum {
+  BG_E_ARG = -1,        /* bad argument (null pointer, capacity too small, unknown mode) */
+  BG_E_HIP = -2,        /* HIP runtime failure */
+  BG_E_NOMEM = -3,      /* device or host allocation failed */
+  BG_E_SCORE_RANGE = -4,/* a substitution score minus the gap-open penalty does not fit int16 */
+  BG_E_NO_BATCH = -5,   /* bg_batch_execute/fetch without a prepared batch */
+  BG_E_ALPHABET = -6    /* more than 32 distinct scorable symbols in one batch */
+};
+
+/* Scoring closure as data: code[byte] in [0, alphabet_size) or 0xFF when the closure would
+ * panic on that byte; table[c1 * 32 + c2] = S(byte1, byte2) with c1 from seq1. */
+typedef struct bg_scoring {
+  int32_t alphabet_size;
+  uint8_t code[256];
+  int32_t table[32 * 32];
+} bg_scoring;
+
+enum { BG_BLOSUM62 = 0, BG_PAM250 = 1, BG_UNIT = 2 };
+
+/* Fills *out with the reference's 26x26 table ('A'..'Z'; other bytes unscorable). */
+int bg_scoring_builtin(int which, bg_scoring* out);
+
+typedef struct bg_aligner bg_aligner;
+
+/* device: HIP device ordinal (one process per GPU).  NULL on failure. */
+bg_aligner* bg_aligner_new(int device);
+void bg_aligner_free(bg_aligner* h);
+
+/* One alignment.  out1/out2 receive the aligned strings ('-' for gaps), both *out_len bytes;
+ * cap must be >= n1 + n2.  Returns a BG_* status (>= 0) or a BG_E_* error (< 0). */
+int bg_align(bg_aligner* h, int mode, const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2,
+             const bg_scoring* scoring, int32_t a, int32_t b, int32_t* score, uint8_t* out1,
+             uint8_t* out2, size_t cap, size_t* out_len);
+
+typedef struct bg_pair_result {
+  int32_t status;    /* BG_* */
+  int32_t score;
+  uint64_t offset;   /* pair p's strings are at out1+offset / out2+offset; offset = sum_{q<p} (n1_q+n2_q) */
+  uint32_t len;      /* aligned length */
+  uint32_t end_i;    /* DP cell the traceback started from */
+  uint32_t end_j;
+  uint32_t start1;   /* cell (start1, start2) where the traceback walk stopped */
+  uint32_t start2;
+  uint32_t reserved;
+} bg_pair_result;
+
+/* Many independent pairs with one mode / scoring / (a, b) — the batched form of one
+ * SequenceAligner::*_alignment call.  out1/out2 capacity >= sum(n1+n2).  Returns 0 or BG_E_*. */
+int bg_align_batch(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
+                   const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                   const bg_scoring* scoring, int32_t a, int32_t b, bg_pair_result* results,
+                   uint8_t* out1, uint8_t* out2, size_t out_cap);
+
+/* Split form of bg_align_batch for callers that keep inputs resident on the device:
+ * prepare (validate, plan, upload) once, execute (enqueue DP + end cell + traceback on the
+ * handle's stream; async) any number of times, fetch (wait, download, unpack). */
+int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
+                     const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                     const bg_scoring* scoring, int32_t a, int32_t b);
+int bg_batch_execute(bg_aligner* h);
+int bg_batch_fetch(bg_aligner* h, bg_pair_result* results, uint8_t* out1, uint8_t* out2,
+                   size_t out_cap);
+/* Blocks until the enqueued work is done. */
+int bg_synchronize(bg_aligner* h);
+
+typedef struct bg_stats {
+  uint64_t cells;          /* sum n1*n2 of the prepared batch */
+  uint64_t trace_bytes;    /* trace arena bytes written per execute */
+  uint64_t boundary_bytes; /* strip-boundary bytes written per execute */
+  uint64_t residue_bytes;  /* seq1+seq2 bytes */
+  uint64_t device_bytes;   /* device memory held by the handle */
+  int32_t R;               /* rows per lane */
+  int32_t waves;           /* waves per workgroup (one workgroup per pair) */
+  int32_t affine;          /* 1: affine kernel (open < extend), 0: linear-gap kernel */
+  int32_t dna;             /* 1: register profile (<= 4 symbols), 0: LDS profile */
+  int32_t local;
+  int32_t npairs;
+  float dp_ms;             /* last execute: DP kernel time (HIP events on the handle's stream) */
+  float finish_ms;         /* last execute: end-cell + traceback kernel time */
+} bg_stats;
+
+int bg_get_stats(bg_aligner* h, bg_stats* out);
+
+/* Tuning overrides for tests/benchmarks (0 = automatic). */
+int bg_set_tuning(bg_aligner* h, int R, int waves);
+
+const char* bg_status_string(int status);
+int bg_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BIOGARDEN_GPU_H */

@@ -264,9 +264,11 @@ static int32_t run_mode(or_aligner* A, int mode, const uint8_t* s1, size_t n1, c
   switch (mode) {
     case OR_GLOBAL: {                                          /* aligner.rs:84-121 */
       maybe_resize(A, n1, n2);
-      A->m[IX(A, 0, 1)] = a;
+      /* exact mode restricts the border writes to the pair's region: row0[1] / col0[1] of an
+       * exactly (n1+1)x(n2+1) scratch do not exist when n2 == 0 / n1 == 0 */
+      if (!(A->exact && n2 == 0)) A->m[IX(A, 0, 1)] = a;
       for (size_t j = 2; j < n2 + 1; ++j) A->m[IX(A, 0, j)] = wadd(A->m[IX(A, 0, j - 1)], b);
-      A->m[IX(A, 1, 0)] = a;
+      if (!(A->exact && n1 == 0)) A->m[IX(A, 1, 0)] = a;
       for (size_t i = 2; i < n1 + 1; ++i) A->m[IX(A, i, 0)] = wadd(A->m[IX(A, i - 1, 0)], b);
       trace_borders(A);
       dp(A, s1, n1, s2, n2, sc, a, b, 0);
@@ -295,7 +297,7 @@ static int32_t run_mode(or_aligner* A, int mode, const uint8_t* s1, size_t n1, c
     case OR_FITTING: {                                         /* :216-260 */
       maybe_resize(A, n1, n2);
       memset(A->m, 0, A->rows * A->cols * 4);
-      A->m[IX(A, 0, 1)] = a;
+      if (!(A->exact && n2 == 0)) A->m[IX(A, 0, 1)] = a;
       for (size_t j = 2; j < n2 + 1; ++j) A->m[IX(A, 0, j)] = wadd(A->m[IX(A, 0, j - 1)], b);
       trace_borders(A);
       dp(A, s1, n1, s2, n2, sc, a, b, 0);

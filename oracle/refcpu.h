@@ -12,8 +12,9 @@
  *   - every matrix access is bounds-checked like ndarray (an out-of-bounds index = panic)
  *   - release-mode integer semantics: wrapping i32 adds, saturating add on the extend term
  * so it reproduces the reference's panics/hangs as status codes.  An "exact" aligner instead
- * allocates exactly (len1+1)x(len2+1) fresh buffers per call: the product's documented
- * semantics (DESIGN.md "Buffer semantics"), equal to the reference wherever it returns.
+ * allocates exactly (len1+1)x(len2+1) fresh buffers per call (border writes restricted to that
+ * region): the product's documented semantics (DESIGN.md "Buffer semantics"), equal to the
+ * reference wherever it returns.
  *
  * Parity pinning: the restatement reproduces the reference's 5 integration goldens
  * (tests/integration.rs:234-312, fixtures tests/golden/reference_fixtures/) and the 5 aligner

@@ -1,0 +1,243 @@
+"""Parity of the HIP path (libbiogarden_gpu.so through the C ABI) with the reference.
+
+* the reference's own integration goldens and doctests, through the SequenceAligner mirror
+  (reads like tests/integration.rs:234-312);
+* seeded random pairs against the CPU oracle (oracle/refcpu.c) — bit-exact score and strings —
+  over every mode, a<b / a=b / a>b, DNA / protein, edge lengths, and every kernel geometry;
+* the fresh-aligner reference model: wherever the reference returns, so do we, identically;
+  wherever it panics/hangs we flag it (status 3/4);
+* full BASELINE size (10 kbp x 10 kbp semiglobal, blosum62 -1/-2) through size-independent
+  properties, plus two full pairs against the oracle.
+"""
+import os
+import random
+
+import pytest
+
+from conftest import REF_FIX, REFERENCE_DOCTESTS, REFERENCE_GOLDENS, read_fasta
+
+pytestmark = pytest.mark.gpu
+
+DNA = b"ACGT"
+PROT = b"ACDEFGHIKLMNPQRSTVWY"
+
+
+@pytest.fixture(scope="module")
+def aligner():
+    from biogarden_amd.alignment.aligner import SequenceAligner
+    al = SequenceAligner(0)
+    yield al
+    al.close()
+
+
+def rand_seq(rng, n, alpha):
+    return bytes(rng.choice(alpha) for _ in range(n))
+
+
+def mutate(rng, s, alpha, rate=0.1):
+    out = bytearray()
+    for ch in s:
+        r = rng.random()
+        if r < rate / 3:
+            continue                                   # deletion
+        if r < 2 * rate / 3:
+            out.append(rng.choice(alpha))              # insertion
+        out.append(rng.choice(alpha) if rng.random() < rate / 3 else ch)
+    return bytes(out)
+
+
+def check_batch(aligner, oracle, mode, pairs, scoring, a, b, fresh=True):
+    from biogarden_amd.alignment import score as score_mod
+    res = aligner.align_batch(mode, pairs, getattr(score_mod, scoring), a, b)
+    bad = []
+    for (s1, s2), r in zip(pairs, res):
+        st, sc, o1, o2 = oracle.align(mode, s1, s2, scoring, a, b, exact=True)
+        got = (r.status, r[0], bytes(r[1].chain), bytes(r[2].chain))
+        if st == 0 and r.status in (0, 4) and got[1:] == (sc, o1, o2):
+            pass                                     # same answer (4 = fresh reference differs)
+        elif st in (4, 5) and r.status == 4:
+            pass                                     # the reference panics: flagged
+        elif st == r.status and st in (1, 2, 3):
+            pass
+        else:
+            bad.append((len(s1), len(s2), s1[:40], s2[:40], (st, sc), got[:2]))
+        if fresh:
+            fst, fsc, f1, f2 = oracle.align(mode, s1, s2, scoring, a, b, exact=False)
+            if fst == 0 and st == 0 and (fsc, f1, f2) != (sc, o1, o2):
+                # the fresh reference answers from stale scratch beyond the pair (history
+                # dependent, A.7): we return the exact-size answer and flag it
+                if r.status != 4:
+                    bad.append(("stale-not-flagged", len(s1), len(s2), r.status))
+            elif fst == 0:
+                if not (r.status == 0 and (r[0], bytes(r[1].chain), bytes(r[2].chain)) == (fsc, f1, f2)):
+                    bad.append(("fresh-ok", len(s1), len(s2), fst, r.status, fsc, r[0]))
+            elif r.status == 0:
+                bad.append(("fresh-panics-but-ok", len(s1), len(s2), fst, s1[:30], s2[:30]))
+    assert not bad, bad[:5]
+    return res
+
+
+# ------------------------------------------------------------------ reference goldens
+
+
+@pytest.mark.parametrize("mode,scoring,a,b,expected", REFERENCE_GOLDENS)
+def test_integration_golden(aligner, mode, scoring, a, b, expected):
+    from biogarden_amd.alignment import score
+    from biogarden_amd.io import fasta
+    inputs = fasta.read_tile(os.path.join(REF_FIX, "input", "%s_alignment.fasta" % mode))
+    outputs = fasta.read_tile(os.path.join(REF_FIX, "output", "%s_alignment.fasta" % mode))
+    fn = getattr(aligner, "%s_alignment" % mode)
+    align_score, s1_aligned, s2_aligned = fn(inputs[0], inputs[1], getattr(score, scoring), a, b)
+    assert align_score == expected
+    assert s1_aligned == outputs[0]
+    assert s2_aligned == outputs[1]
+
+
+@pytest.mark.parametrize("case", REFERENCE_DOCTESTS, ids=lambda c: c[0])
+def test_doctest(aligner, case):
+    from biogarden_amd.alignment import score
+    from biogarden_amd.ds import Sequence
+    mode, s1, s2, scoring, a, b, exp, e1, e2 = case
+    fn = getattr(aligner, "%s_alignment" % mode)
+    got = fn(Sequence(s1), Sequence(s2), getattr(score, scoring), a, b)
+    assert got == (exp, Sequence(e1), Sequence(e2))
+
+
+def test_errors_like_reference(aligner):
+    from biogarden_amd.alignment import score
+    from biogarden_amd.error import InvalidArgumentRange, InvalidInputSize, ReferencePanic
+    with pytest.raises(InvalidArgumentRange):
+        aligner.global_alignment(b"AC", b"AC", score.unit, 1, -1)
+    with pytest.raises(InvalidArgumentRange):
+        aligner.local_alignment(b"AC", b"AC", score.unit, -1, 1)
+    with pytest.raises(InvalidInputSize):
+        aligner.fitting_alignment(b"A", b"AC", score.unit, -1, -1)
+    with pytest.raises(ReferencePanic):
+        aligner.global_alignment(b"Ac", b"AC", score.unit, -1, -1)
+    assert aligner.semiglobal_alignment(b"GGACGT", b"ACGTCC", score.unit, -1, -1) == (4, b"ACGT--", b"ACGTCC")
+
+
+def test_custom_closure(aligner, oracle):
+    """An arbitrary scoring closure is tabulated (A.8) and matches the oracle on its table."""
+    def match_mismatch(x, y):
+        return 3 if x == y else -2
+    s1, s2 = b"ACGTTGCAACG", b"ACGTGCATACG"
+    got = aligner.global_alignment(s1, s2, match_mismatch, -4, -1)
+    sc = oracle.scoring(match_mismatch)
+    st, score, o1, o2 = oracle.align("global", s1, s2, sc, -4, -1, exact=True)
+    assert st == 0 and got == (score, o1, o2)
+
+
+# ------------------------------------------------------------------ seeded random vs oracle
+
+GAPS = [(-11, -1), (-2, -2), (-1, -2), (-3, -1), (0, 0), (-5, -5)]
+
+
+@pytest.mark.parametrize("mode", ["global", "local", "fitting", "overlap", "semiglobal"])
+@pytest.mark.parametrize("alpha,scoring", [(DNA, "blosum62"), (DNA, "unit"), (PROT, "blosum62"), (PROT, "pam250")])
+def test_random_small(aligner, oracle, mode, alpha, scoring):
+    rng = random.Random(hash((mode, alpha, scoring)) & 0xFFFF)
+    lens = [0, 1, 2, 3, 7, 31, 63, 64, 65, 100, 127, 128, 129, 200, 255, 256, 257, 300]
+    for a, b in GAPS:
+        pairs = []
+        for _ in range(24):
+            n1, n2 = rng.choice(lens), rng.choice(lens)
+            if mode == "fitting" and n1 < n2 and rng.random() < 0.8:
+                n1, n2 = n2, n1
+            s1 = rand_seq(rng, n1, alpha)
+            s2 = mutate(rng, s1, alpha)[:n2] if rng.random() < 0.5 else rand_seq(rng, n2, alpha)
+            pairs.append((s1, s2))
+        check_batch(aligner, oracle, mode, pairs, scoring, a, b)
+
+
+@pytest.mark.parametrize("R,W", [(4, 1), (4, 3), (8, 1), (8, 2), (8, 4), (8, 16)])
+@pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("local", -11, -1), ("global", -11, -1), ("overlap", -2, -2)])
+def test_geometries_multistrip(aligner, oracle, R, W, mode, a, b):
+    """Pairs spanning several strips, every pipelining depth; DNA and protein."""
+    rng = random.Random(R * 100 + W + len(mode))
+    aligner.set_tuning(R, W)
+    try:
+        for alpha, scoring in ((DNA, "blosum62"), (PROT, "blosum62")):
+            pairs = []
+            for n1, n2 in ((1500, 1400), (700, 2100), (513, 64), (2049, 511), (64 * R * 3, 333), (1, 900)):
+                s1 = rand_seq(rng, n1, alpha)
+                s2 = mutate(rng, s1, alpha, 0.15)[:n2]
+                pairs.append((s1, s2))
+            check_batch(aligner, oracle, mode, pairs, scoring, a, b, fresh=False)
+    finally:
+        aligner.set_tuning(0, 0)
+
+
+def test_buffer_edge_and_divergence(aligner, oracle):
+    """Lengths around the reference's 1024x1024 default scratch (A.7)."""
+    rng = random.Random(7)
+    for mode, a, b in (("global", -11, -1), ("semiglobal", -1, -1), ("overlap", -2, -2),
+                       ("fitting", -1, -1), ("local", -11, -1)):
+        pairs = []
+        for n1, n2 in ((1024, 10), (10, 1024), (1023, 1023), (1025, 17), (0, 1024), (1024, 0), (1024, 1024)):
+            pairs.append((rand_seq(rng, n1, DNA), rand_seq(rng, n2, DNA)))
+        check_batch(aligner, oracle, mode, pairs, "unit", a, b)
+
+
+def test_unscorable_and_empty(aligner, oracle):
+    pairs = [(b"ACGT", b"ACXT"), (b"acgt", b"ACGT"), (b"", b"ACGT"), (b"ACGT", b""), (b"", b""),
+             (b"A-C", b"AC")]
+    for mode in ("global", "local", "semiglobal", "overlap"):
+        check_batch(aligner, oracle, mode, pairs, "blosum62", -3, -1)
+
+
+# ------------------------------------------------------------------ BASELINE-size properties
+
+
+def rescore_semiglobal(r, s1, s2, table, a):
+    """Score of the emitted alignment under the linear model (a >= b): end gaps
+    free, every other gap column costs a."""
+    n1, n2 = len(s1), len(s2)
+    ei, ej = r.end
+    k0, l0 = r.start
+    colcase = ei < n1
+    a1, a2 = bytes(r[1].chain), bytes(r[2].chain)
+    tail = (n1 - ei) if colcase else (n2 - ej)
+    pre = k0 if colcase else l0
+    core1, core2 = a1[pre:len(a1) - tail], a2[pre:len(a2) - tail]
+    sc = 0
+    for x, y in zip(core1, core2):
+        if x == 45 or y == 45:
+            sc += a
+        else:
+            sc += table[x - 65][y - 65]
+    degap1 = a1.replace(b"-", b"")
+    degap2 = a2.replace(b"-", b"")
+    return sc, degap1, degap2
+
+
+def test_baseline_size_semiglobal_properties(aligner, oracle):
+    from biogarden_amd.alignment import score
+    rng = random.Random(0xB10A11F0)
+    pairs = []
+    for p in range(8):
+        s1 = rand_seq(rng, 10000, DNA)
+        s2 = mutate(rng, s1, DNA, 0.2)[:10000] if p % 2 else rand_seq(rng, 10000, DNA)
+        pairs.append((s1, s2))
+    res = aligner.align_batch("semiglobal", pairs, score.blosum62, -1, -2)
+    table = score.blosum62.table()
+    for (s1, s2), r in zip(pairs, res):
+        assert r.status == 0
+        sc, d1, d2 = rescore_semiglobal(r, s1, s2, table, -1)
+        assert sc == r[0]
+        assert len(r[1]) == len(r[2])
+        assert d1 == s1[r.start[0] if r.end[0] == len(s1) else 0:]
+        assert s2.endswith(d2)
+    # two full pairs bit-exact against the oracle (1e8 cells each)
+    for (s1, s2), r in list(zip(pairs, res))[:2]:
+        st, sc, o1, o2 = oracle.align("semiglobal", s1, s2, "blosum62", -1, -2, exact=True)
+        assert (st, sc, o1, o2) == (0, r[0], bytes(r[1].chain), bytes(r[2].chain))
+
+
+def test_deterministic(aligner):
+    from biogarden_amd.alignment import score
+    rng = random.Random(3)
+    pairs = [(rand_seq(rng, 3000, DNA), rand_seq(rng, 2500, DNA)) for _ in range(4)]
+    r1 = aligner.align_batch("local", pairs, score.blosum62, -11, -1)
+    r2 = aligner.align_batch("local", pairs, score.blosum62, -11, -1)
+    assert [(x[0], x[1], x[2]) for x in r1] == [(x[0], x[1], x[2]) for x in r2]

@@ -1,0 +1,83 @@
+"""The CPU oracle (oracle/refcpu.c) against every golden the reference's own tests hold.
+
+This pins the restatement before it is trusted as the GPU checker: the 5 integration goldens
+(tests/integration.rs:234-312 + tests/data/{input,output}/*_alignment.fasta) and the 5 aligner
+doctests must be reproduced byte for byte, by both the reference-faithful (fresh 1024x1024
+scratch) and the exact-size aligner.
+"""
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN, REF_FIX, REFERENCE_DOCTESTS, REFERENCE_GOLDENS, read_fasta
+
+
+@pytest.mark.parametrize("mode,scoring,a,b,expected", REFERENCE_GOLDENS)
+@pytest.mark.parametrize("exact", [False, True])
+def test_integration_goldens(oracle, mode, scoring, a, b, expected, exact):
+    inp = read_fasta(os.path.join(REF_FIX, "input", "%s_alignment.fasta" % mode))
+    out = read_fasta(os.path.join(REF_FIX, "output", "%s_alignment.fasta" % mode))
+    st, score, a1, a2 = oracle.align(mode, inp[0][1], inp[1][1], scoring, a, b, exact=exact)
+    assert st == 0
+    assert score == expected
+    assert a1 == out[0][1]
+    assert a2 == out[1][1]
+
+
+@pytest.mark.parametrize("case", REFERENCE_DOCTESTS, ids=lambda c: c[0])
+def test_doctests(oracle, case):
+    mode, s1, s2, scoring, a, b, exp, e1, e2 = case
+    for exact in (False, True):
+        st, score, a1, a2 = oracle.align(mode, s1, s2, scoring, a, b, exact=exact)
+        assert (st, score, a1, a2) == (0, exp, e1, e2)
+
+
+def test_semiglobal_prefix_drop(oracle):
+    # the row case stopping at l == 0 drops seq1's prefix "GG"
+    assert oracle.align("semiglobal", b"GGACGT", b"ACGTCC", "unit", -1, -1) == \
+        (0, 4, b"ACGT--", b"ACGTCC")
+
+
+def test_reference_errors(oracle):
+    assert oracle.align("global", b"AC", b"AC", "unit", 1, -1)[0] == 1      # InvalidArgumentRange
+    assert oracle.align("local", b"AC", b"AC", "unit", -1, 2)[0] == 1
+    assert oracle.align("fitting", b"A", b"AC", "unit", -1, -1)[0] == 2     # InvalidInputSize
+    assert oracle.align("semiglobal", b"AC", b"AC", "unit", 1, 1)[0] == 0   # no validation
+    assert oracle.align("global", b"Ac", b"AC", "unit", -1, -1)[0] == 3     # score panic
+    # len == buffer dim on a fresh (1024x1024) aligner panics; the exact aligner answers
+    s = b"A" * 1024
+    assert oracle.align("global", s, b"AC", "unit", -1, -1)[0] == 4
+    assert oracle.align("global", s, b"AC", "unit", -1, -1, exact=True)[0] == 0
+
+
+def test_tables_agree():
+    """Product tables (bg_tables.inc), oracle tables and the golden JSON are one data set."""
+    from oracle import refcpu
+    with open(os.path.join(GOLDEN, "score_tables.json")) as f:
+        gold = json.load(f)["tables"]
+    for name in ("blosum62", "pam250", "unit"):
+        sc = refcpu.scoring(name)
+        for r in range(26):
+            for c in range(26):
+                assert sc.table[r * 32 + c] == gold[name][r][c]
+    # product decode (pure host code, no GPU needed)
+    from biogarden_amd import _native
+    for name, which in (("blosum62", 0), ("pam250", 1), ("unit", 2)):
+        sc = _native.builtin_scoring(which)
+        assert sc.alphabet_size == 26
+        for r in range(26):
+            for c in range(26):
+                assert sc.table[r * 32 + c] == gold[name][r][c], (name, r, c)
+        assert sc.code[ord("A")] == 0 and sc.code[ord("Z")] == 25 and sc.code[ord("a")] == 0xFF
+
+
+def test_blosum62_dna_block():
+    """the DNA sub-block of the reference BLOSUM62."""
+    with open(os.path.join(GOLDEN, "score_tables.json")) as f:
+        b = json.load(f)["tables"]["blosum62"]
+    ix = {ch: ord(ch) - 65 for ch in "ACGT"}
+    want = {"AA": 4, "CC": 9, "GG": 6, "TT": 5, "AC": 0, "AG": 0, "AT": 0, "CG": -3, "CT": -1,
+            "GT": -2}
+    for k, v in want.items():
+        assert b[ix[k[0]]][ix[k[1]]] == v == b[ix[k[1]]][ix[k[0]]]
