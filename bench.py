@@ -1,0 +1,223 @@
+#!/usr/bin/env python3
+"""Benchmark: GCUPS of 10 kbp x 10 kbp affine-gap semiglobal alignment on MI355X.
+
+Metric (BASELINE.json): "GCUPS (billion DP cells/s), 10k x 10k affine-gap semiglobal, 1/2/4/8
+MI355X".  Workload per GPU: 256 synthetic uniform-DNA pairs of 10,000 x 10,000, semiglobal,
+BLOSUM62, gap open -1 / extend -2 (the reference's own config-1 parameters,
+examples/from_file.rs:19-32).  One step = one pass of the hot path over the batch with the
+inputs resident in HBM: DP kernel (scores + trace) -> end-cell search -> traceback writing both
+aligned strings (aligner.rs:351-435).  Every rank aligns its own 256 pairs (weak scaling: the
+pairs are independent, no data-path collective); after the timed region the per-rank results
+are gathered to rank 0 over RCCL (reported as gather_ms).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
+SEED = 0xB10A11F0 + 5          # seed = 0xB10A11F0 + config index (metric = 5)
+
+
+def make_pairs(npairs, n1, n2, seed):
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    pairs = []
+    for _ in range(npairs):
+        s1 = acgt[rng.integers(0, 4, n1)].tobytes()
+        s2 = acgt[rng.integers(0, 4, n2)].tobytes()
+        pairs.append((s1, s2))
+    return pairs
+
+
+def cpu_baseline(pairs, mode, a, b, threads):
+    """The oracle (C restatement of the reference with its six full matrices) on host cores."""
+    from oracle import refcpu
+    secs, scores, sts = refcpu.align_batch(mode, pairs, "blosum62", a, b, nthreads=threads,
+                                           exact=False)
+    cells = sum(len(x) * len(y) for x, y in pairs)
+    return cells / secs / 1e9, secs, scores, sts
+
+
+def load_pmc_traffic(workload):
+    """HBM bytes per DP launch from the committed rocprofv3 PMC summary for this workload
+    (profiles/pmc_<workload>.json, written by tools/profile.sh), else None."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
+    if not os.path.exists(path):
+        return None
+    try:
+        with open(path) as f:
+            return json.load(f).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--pairs", type=int, default=256)
+    ap.add_argument("--len1", type=int, default=10000)
+    ap.add_argument("--len2", type=int, default=10000)
+    ap.add_argument("--mode", default="semiglobal")
+    ap.add_argument("--open", type=int, default=-1)
+    ap.add_argument("--extend", type=int, default=-2)
+    ap.add_argument("--R", type=int, default=0)
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--cpu-pairs", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-gather", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from biogarden_amd import _native
+
+    h = _native.Handle(local_rank)
+    if args.R or args.waves:
+        h.set_tuning(args.R, args.waves)
+    pairs = make_pairs(args.pairs, args.len1, args.len2, SEED + 1000003 * rank)
+    sc = _native.builtin_scoring(_native.BG_BLOSUM62)
+    h.prepare(args.mode, pairs, sc, args.open, args.extend)
+    st = h.stats()
+    cells = st["cells"]
+
+    for _ in range(args.warmup):
+        h.execute()
+    h.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    barrier()
+    h.profile_begin()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        h.execute()
+    h.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    dp_ms, fin_ms, nexec = h.profile_end()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_cells = cells * world
+    gcups = total_cells * args.steps / elapsed / 1e9
+
+    # ---- results: RCCL gather of every rank's packed results to rank 0
+    gather_ms = None
+    results0 = None
+    nbytes = h.export_size()
+    local = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    h.export_to(local.data_ptr(), nbytes)
+    if dist is not None and not args.no_gather:
+        sizes = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
+        dist.all_gather(sizes, torch.tensor([nbytes], dtype=torch.int64, device="cuda"))
+        mx = int(max(s.item() for s in sizes))
+        buf = torch.zeros(mx, dtype=torch.uint8, device="cuda")
+        buf[:nbytes] = local
+        barrier()
+        tg = time.perf_counter()
+        gl = [torch.empty(mx, dtype=torch.uint8, device="cuda") for _ in range(world)] if rank == 0 else None
+        dist.gather(buf, gl, dst=0)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - tg) * 1e3
+        if rank == 0:
+            results0 = [_native.decode_export(g[:int(s.item())].cpu().numpy().tobytes())
+                        for g, s in zip(gl, sizes)]
+    else:
+        results0 = [_native.decode_export(local.cpu().numpy().tobytes())]
+
+    if rank != 0:
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    ok_status = all(r["status"] == 0 for rr in results0 for r in rr)
+
+    # ---- roofline of the DP kernel (algorithmic bytes per launch / event-timed duration)
+    bytes_per_cell = 0.25 if st["affine"] == 0 else 0.5
+    algo_bytes = cells * bytes_per_cell + st["residue_bytes"]
+    achieved = algo_bytes / (dp_ms * 1e-3) / 1e9 if dp_ms > 0 else 0.0
+    ops_per_cell = 10 if st["affine"] == 0 else 18
+    valu_achieved = ops_per_cell * cells / (dp_ms * 1e-3) if dp_ms > 0 else 0.0
+    workload = "semiglobal_%dx%dx%d_blosum62_o%d_e%d" % (args.pairs, args.len1, args.len2,
+                                                          -args.open, -args.extend)
+    traffic = load_pmc_traffic(workload)
+
+    # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0 only)
+    cpu = None
+    if not args.no_cpu and world == 1:
+        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
+                             os.cpu_count() or 1))
+        sample = pairs[:max(1, min(args.cpu_pairs, len(pairs)))]
+        rate, secs, cscores, csts = cpu_baseline(sample, args.mode, args.open, args.extend, threads)
+        gscores = [r["score"] for r in results0[0][:len(sample)]]
+        cpu = {"value": round(rate, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
+               "sample": "%d of the %d pairs (%dx%d), oracle/refcpu.c reference-faithful full "
+                         "matrices, one aligner per thread, %.1f s wall" % (
+                             len(sample), len(pairs), args.len1, args.len2, secs),
+               "scores_match_gpu": "%d/%d" % (sum(int(x == y) for x, y in zip(cscores, gscores)),
+                                               len(sample))}
+
+    line = {
+        "metric": "GCUPS (billion DP cells/s), 10k×10k affine-gap semiglobal, 1/2/4/8 MI355X",
+        "value": round(gcups, 3),
+        "unit": "GCUPS",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (uniform DNA, numpy PCG64 seed 0x%X + 1000003*rank)" % SEED,
+        "config": {"workload": workload, "pairs_per_gpu": args.pairs, "len1": args.len1,
+                   "len2": args.len2, "mode": args.mode, "scoring": "blosum62",
+                   "gap_open": args.open, "gap_extend": args.extend,
+                   "kernel": {"R": st["R"], "waves": st["waves"], "affine": st["affine"],
+                              "dna_profile": st["dna"]},
+                   "parallelism": "dp%d (independent pairs per rank)" % world},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic,
+                     "algorithmic_bytes_per_launch": int(algo_bytes),
+                     "kernel_ms": round(dp_ms, 4), "finish_ms": round(fin_ms, 4),
+                     "valu": {"achieved_ops": valu_achieved, "peak_ops": VALU_PEAK_OPS,
+                              "frac": round(valu_achieved / VALU_PEAK_OPS, 4),
+                              "ops_per_cell_model": ops_per_cell}},
+        "cpu_baseline": cpu,
+        "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+        "all_status_ok": ok_status,
+    }
+    print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -19,7 +19,7 @@ BG_BLOSUM62, BG_PAM250, BG_UNIT = range(3)
 EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align",
            "bg_align_batch", "bg_batch_prepare", "bg_batch_execute", "bg_batch_fetch",
            "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
-           "bg_abi_version"]
+           "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -88,6 +88,11 @@ def lib():
     L.bg_status_string.argtypes = [ctypes.c_int]
     L.bg_status_string.restype = ctypes.c_char_p
     L.bg_abi_version.restype = ctypes.c_int
+    L.bg_profile_begin.argtypes = [ctypes.c_void_p]
+    L.bg_profile_end.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                 ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    L.bg_batch_export.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.POINTER(ctypes.c_size_t)]
     _LIB = L
     return L
 
@@ -172,7 +177,46 @@ class Handle:
         self.execute()
         return self.fetch()
 
+    def profile_begin(self):
+        check(lib().bg_profile_begin(self._p))
+
+    def profile_end(self):
+        """-> (avg DP kernel ms, avg finish kernel ms, executes) over the profiled region."""
+        dp, fin, n = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+        check(lib().bg_profile_end(self._p, ctypes.byref(dp), ctypes.byref(fin), ctypes.byref(n)))
+        return dp.value, fin.value, n.value
+
+    def export_size(self):
+        n = ctypes.c_size_t(0)
+        check(lib().bg_batch_export(self._p, None, ctypes.byref(n)))
+        return n.value
+
+    def export_to(self, device_ptr, nbytes):
+        """Packs the last execute's results into device memory at device_ptr (same GPU)."""
+        n = ctypes.c_size_t(nbytes)
+        check(lib().bg_batch_export(self._p, ctypes.c_void_p(device_ptr), ctypes.byref(n)))
+        return n.value
+
     def stats(self):
         st = BgStats()
         check(lib().bg_get_stats(self._p, ctypes.byref(st)))
         return {f: getattr(st, f) for f, _ in BgStats._fields_}
+
+
+def decode_export(buf):
+    """Parses a bg_batch_export record (bytes) -> list of result dicts (for rank 0 after a
+    gather)."""
+    import struct
+    n = struct.unpack_from("<Q", buf, 0)[0]
+    rs = ctypes.sizeof(BgPairResult)
+    recs = [BgPairResult.from_buffer_copy(buf, 8 + i * rs) for i in range(n)]
+    base1 = 8 + n * rs
+    out_bytes = (len(buf) - base1) // 2
+    base2 = base1 + out_bytes
+    out = []
+    for r in recs:
+        out.append({"status": r.status, "score": r.score,
+                    "aligned1": bytes(buf[base1 + r.offset: base1 + r.offset + r.len]),
+                    "aligned2": bytes(buf[base2 + r.offset: base2 + r.offset + r.len]),
+                    "end": (r.end_i, r.end_j), "start": (r.start1, r.start2)})
+    return out

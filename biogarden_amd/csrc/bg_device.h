@@ -26,8 +26,27 @@ struct BgPair {
   int32_t nstrips;     // ceil(n1 / (64 R)); 0 when n1 == 0 or n2 == 0 (no DP cells)
   int32_t pad;         // virtual rows above row 1 in strip 0: nstrips*64R - n1
   int32_t nc;          // chunks per strip: n2/64 + 2
-  int32_t index;       // caller's pair index (results are scattered back to it)
+  int32_t index;       // plan slot (results array index)
+  uint64_t caller_off; // caller's output offset (sum of n1+n2 over earlier caller pairs)
+  int32_t caller;      // caller's pair index
+  int32_t reserved;
 };
+
+// Would a freshly constructed reference SequenceAligner (1024x1024 scratch, aligner.rs:44-55)
+// panic, hang or answer from stale scratch on this pair?  Exact-size semantics differ from it
+// only when it does not resize (both lengths <= 1024) and either indexes row/column 1024 or its
+// end-cell fold reaches cells beyond the pair's region (DESIGN.md "Buffer semantics").
+__host__ __device__ inline bool bg_ref_fresh_divergent(int mode, long n1, long n2, int score) {
+  if (n1 > 1024 || n2 > 1024) return false;  // resized to exactly (n1+1, n2+1)
+  const bool e1 = n1 == 1024, e2 = n2 == 1024;
+  switch (mode) {
+    case BGK_GLOBAL: return e1 || e2;
+    case BGK_LOCAL: return (e1 || e2) && n1 > 0 && n2 > 0;
+    case BGK_FITTING: return e2 || (e1 && n2 > 0) || (score < 0 && n1 + 1 < 1024);
+    case BGK_OVERLAP: return e1 || e2 || (score <= 0 && n2 + 1 < 1024);
+    default: return e1 || e2 || (score == 0 && n2 + 1 < 1024);
+  }
+}
 
 // Per-pair result written by the finish kernel.
 struct BgResult {
@@ -71,3 +90,23 @@ struct BgFinishArgs {
   int32_t affine;          // trace carries x/y bits
   int32_t npairs;
 };
+
+// bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.
+struct BgPairResultDev {
+  int32_t status, score;
+  uint64_t offset;
+  uint32_t len, end_i, end_j, start1, start2, reserved;
+};
+
+struct BgExportArgs {
+  const BgPair* pairs;
+  const BgResult* results;
+  const uint8_t* out1;
+  const uint8_t* out2;
+  uint8_t* dst;            // [u64 n][BgPairResultDev x n][aligned1 bytes][aligned2 bytes]
+  uint64_t npairs_caller;
+  uint64_t out_bytes;      // sum over caller pairs of n1+n2
+  int32_t mode;
+};
+
+

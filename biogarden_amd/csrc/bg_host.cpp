@@ -21,6 +21,7 @@
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
 extern "C" void* bg_finish_kernel_ptr();
+extern "C" void* bg_export_kernel_ptr();
 
 #include "bg_tables.inc"
 
@@ -56,7 +57,12 @@ struct bg_aligner {
   int cus = 256;
   hipStream_t stream = nullptr;
   hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  DevBuf seq1, seq2, lut, prof, pairs, trace, bndM, bndX, aux, out1, out2, results;
+  DevBuf seq1, seq2, lut, prof, pairs, trace, bndM, bndX, aux, out1, out2, results, recs;
+
+  // profiling ring (bg_profile_begin/end)
+  std::vector<hipEvent_t> ring;
+  bool profiling = false;
+  int ringUsed = 0;
 
   // prepared batch
   bool prepared = false;
@@ -80,7 +86,7 @@ struct bg_aligner {
 
   size_t device_bytes() const {
     return seq1.cap + seq2.cap + lut.cap + prof.cap + pairs.cap + trace.cap + bndM.cap +
-           bndX.cap + aux.cap + out1.cap + out2.cap + results.cap;
+           bndX.cap + aux.cap + out1.cap + out2.cap + results.cap + recs.cap;
   }
 };
 
@@ -143,9 +149,11 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   for (DevBuf* d : {&h->seq1, &h->seq2, &h->lut, &h->prof, &h->pairs, &h->trace, &h->bndM, &h->bndX,
-                    &h->aux, &h->out1, &h->out2, &h->results})
+                    &h->aux, &h->out1, &h->out2, &h->results, &h->recs})
     d->release();
   for (auto& e : h->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : h->ring)
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -288,6 +296,8 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     P.n1 = (int32_t)n1[p];
     P.n2 = (int32_t)n2[p];
     P.index = (int32_t)h->plan.size();
+    P.caller = (int32_t)p;
+    P.caller_off = h->outoff[p];
     P.off1 = o1; o1 += n1[p];
     P.off2 = o2; o2 += n2[p];
     const bool dp = n1[p] > 0 && n2[p] > 0;
@@ -356,6 +366,18 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   if (!h->plan.empty())
     BG_HIP(hipMemcpyAsync(h->pairs.p, h->plan.data(), sizeof(BgPair) * h->plan.size(),
                           hipMemcpyHostToDevice, h->stream));
+  {
+    std::vector<BgPairResultDev> tmpl(npairs);
+    for (size_t p = 0; p < npairs; ++p) {
+      std::memset(&tmpl[p], 0, sizeof(tmpl[p]));
+      tmpl[p].status = h->prestatus[p] < 0 ? 0 : h->prestatus[p];
+      tmpl[p].offset = h->outoff[p];
+    }
+    if (!h->recs.ensure(sizeof(BgPairResultDev) * (npairs + 1))) return BG_E_NOMEM;
+    if (npairs)
+      BG_HIP(hipMemcpyAsync(h->recs.p, tmpl.data(), sizeof(BgPairResultDev) * npairs,
+                            hipMemcpyHostToDevice, h->stream));
+  }
   BG_HIP(hipStreamSynchronize(h->stream));
   h->order_ = order;
   h->prepared = true;
@@ -367,7 +389,14 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   if (!h->prepared) return BG_E_NO_BATCH;
   BG_HIP(hipSetDevice(h->device));
   const unsigned np = (unsigned)h->plan.size();
-  BG_HIP(hipEventRecord(h->ev[0], h->stream));
+  hipEvent_t e0 = h->ev[0], e1 = h->ev[1], e2 = h->ev[2];
+  if (h->profiling && h->ringUsed + 3 <= (int)h->ring.size()) {
+    e0 = h->ring[h->ringUsed];
+    e1 = h->ring[h->ringUsed + 1];
+    e2 = h->ring[h->ringUsed + 2];
+    h->ringUsed += 3;
+  }
+  BG_HIP(hipEventRecord(e0, h->stream));
   if (np) {
     void* fn = bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
     if (!fn) return BG_E_ARG;
@@ -389,7 +418,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     void* args[] = {&A};
     BG_HIP(hipLaunchKernel(fn, dim3(np), dim3(64 * h->W), args, h->lds, h->stream));
   }
-  BG_HIP(hipEventRecord(h->ev[1], h->stream));
+  BG_HIP(hipEventRecord(e1, h->stream));
   if (np) {
     BgFinishArgs F;
     F.pairs = h->pairs.as<BgPair>();
@@ -410,7 +439,10 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     void* args[] = {&F};
     BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(), dim3(np), dim3(64), args, 0, h->stream));
   }
-  BG_HIP(hipEventRecord(h->ev[2], h->stream));
+  BG_HIP(hipEventRecord(e2, h->stream));
+  if (e0 != h->ev[0]) {  // keep ev[] meaning "last execute" for bg_get_stats
+    h->ev[0] = e0; h->ev[1] = e1; h->ev[2] = e2;
+  }
   h->executed = true;
   return BG_OK;
 }
@@ -424,22 +456,6 @@ extern "C" int bg_synchronize(bg_aligner* h) {
     (void)hipEventElapsedTime(&h->fin_ms, h->ev[1], h->ev[2]);
   }
   return BG_OK;
-}
-
-// Would a freshly constructed reference SequenceAligner (1024x1024 scratch, aligner.rs:44-55)
-// panic, hang or answer differently on this pair?  Exact-size semantics differ from it only when
-// it does not resize (both lengths <= 1024) and either indexes row/column 1024 or its end-cell
-// fold reaches stale cells beyond the pair's region (DESIGN.md "Buffer semantics").
-static bool ref_fresh_divergent(int mode, size_t n1, size_t n2, int32_t score) {
-  if (n1 > 1024 || n2 > 1024) return false;  // resized to exactly (n1+1, n2+1)
-  const bool edge1 = n1 == 1024, edge2 = n2 == 1024;
-  switch (mode) {
-    case BG_GLOBAL: return edge1 || edge2;
-    case BG_LOCAL: return (edge1 || edge2) && n1 > 0 && n2 > 0;
-    case BG_FITTING: return edge2 || (edge1 && n2 > 0) || (score < 0 && n1 + 1 < 1024);
-    case BG_OVERLAP: return edge1 || edge2 || (score <= 0 && n2 + 1 < 1024);
-    default: return edge1 || edge2 || (score == 0 && n2 + 1 < 1024);
-  }
 }
 
 extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1, uint8_t* out2,
@@ -481,7 +497,7 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
     if (r.out_len > (uint32_t)(P.n1 + P.n2) || r.out_start + r.out_len > (uint32_t)(P.n1 + P.n2)) return BG_E_HIP;
     std::memcpy(out1 + h->outoff[p], h->ho1.data() + P.out_off + r.out_start, r.out_len);
     std::memcpy(out2 + h->outoff[p], h->ho2.data() + P.out_off + r.out_start, r.out_len);
-    if (o.status == BG_OK && ref_fresh_divergent(h->mode, h->n1v[p], h->n2v[p], r.score))
+    if (o.status == BG_OK && bg_ref_fresh_divergent(h->mode, (long)h->n1v[p], (long)h->n2v[p], r.score))
       o.status = BG_REF_DIVERGENT;
   }
   return BG_OK;
@@ -528,5 +544,68 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->npairs = (int32_t)h->npairs;
   o->dp_ms = h->dp_ms;
   o->finish_ms = h->fin_ms;
+  return BG_OK;
+}
+
+extern "C" int bg_profile_begin(bg_aligner* h) {
+  if (!h) return BG_E_ARG;
+  BG_HIP(hipSetDevice(h->device));
+  if (h->ring.empty()) {
+    h->ring.resize(3 * 4096 + 3, nullptr);
+    for (auto& e : h->ring) BG_HIP(hipEventCreate(&e));
+  }
+  h->profiling = true;
+  h->ringUsed = 0;
+  return BG_OK;
+}
+
+extern "C" int bg_profile_end(bg_aligner* h, float* avg_dp, float* avg_fin, int* n) {
+  if (!h) return BG_E_ARG;
+  BG_HIP(hipSetDevice(h->device));
+  BG_HIP(hipStreamSynchronize(h->stream));
+  double dp = 0, fin = 0;
+  const int cnt = h->ringUsed / 3;
+  for (int i = 0; i < cnt; ++i) {
+    float x = 0, y = 0;
+    BG_HIP(hipEventElapsedTime(&x, h->ring[3 * i], h->ring[3 * i + 1]));
+    BG_HIP(hipEventElapsedTime(&y, h->ring[3 * i + 1], h->ring[3 * i + 2]));
+    dp += x;
+    fin += y;
+  }
+  h->profiling = false;
+  if (avg_dp) *avg_dp = cnt ? (float)(dp / cnt) : 0.f;
+  if (avg_fin) *avg_fin = cnt ? (float)(fin / cnt) : 0.f;
+  if (n) *n = cnt;
+  return BG_OK;
+}
+
+extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
+  if (!h || !bytes) return BG_E_ARG;
+  if (!h->prepared) return BG_E_NO_BATCH;
+  const size_t need = 8 + sizeof(BgPairResultDev) * h->npairs + 2 * h->outBytes;
+  if (!dst) { *bytes = need; return BG_OK; }
+  if (*bytes < need) return BG_E_ARG;
+  if (!h->executed) return BG_E_NO_BATCH;
+  BG_HIP(hipSetDevice(h->device));
+  const uint64_t n = h->npairs;
+  BG_HIP(hipMemcpyAsync(dst, &n, 8, hipMemcpyHostToDevice, h->stream));
+  if (n)
+    BG_HIP(hipMemcpyAsync((uint8_t*)dst + 8, h->recs.p, sizeof(BgPairResultDev) * n,
+                          hipMemcpyDeviceToDevice, h->stream));
+  if (!h->plan.empty()) {
+    BgExportArgs E;
+    E.pairs = h->pairs.as<BgPair>();
+    E.results = h->results.as<BgResult>();
+    E.out1 = h->out1.as<uint8_t>();
+    E.out2 = h->out2.as<uint8_t>();
+    E.dst = (uint8_t*)dst;
+    E.npairs_caller = n;
+    E.out_bytes = h->outBytes;
+    E.mode = h->mode;
+    void* args[] = {&E};
+    BG_HIP(hipLaunchKernel(bg_export_kernel_ptr(), dim3((unsigned)h->plan.size()), dim3(256), args, 0, h->stream));
+  }
+  BG_HIP(hipStreamSynchronize(h->stream));
+  *bytes = need;
   return BG_OK;
 }

@@ -592,6 +592,38 @@ __global__ __launch_bounds__(64) void bg_finish_kernel(BgFinishArgs F) {
   F.results[P.index] = res;
 }
 
+// ------------------------------------------------------------------ export (for collectives)
+
+__global__ __launch_bounds__(256) void bg_export_kernel(BgExportArgs E) {
+  const BgPair& P = E.pairs[blockIdx.x];
+  const BgResult& r = E.results[P.index];
+  BgPairResultDev* recs = reinterpret_cast<BgPairResultDev*>(E.dst + 8);
+  uint8_t* s1 = E.dst + 8 + E.npairs_caller * sizeof(BgPairResultDev);
+  uint8_t* s2 = s1 + E.out_bytes;
+  const uint8_t* src1 = E.out1 + P.out_off + r.out_start;
+  const uint8_t* src2 = E.out2 + P.out_off + r.out_start;
+  for (uint32_t x = threadIdx.x; x < r.out_len; x += blockDim.x) {
+    s1[P.caller_off + x] = src1[x];
+    s2[P.caller_off + x] = src2[x];
+  }
+  if (threadIdx.x == 0) {
+    BgPairResultDev o;
+    o.status = r.status;
+    if (o.status == 0 && bg_ref_fresh_divergent(E.mode, P.n1, P.n2, r.score)) o.status = 4;
+    o.score = r.score;
+    o.offset = P.caller_off;
+    o.len = r.out_len;
+    o.end_i = (uint32_t)r.end_i;
+    o.end_j = (uint32_t)r.end_j;
+    o.start1 = r.start1;
+    o.start2 = r.start2;
+    o.reserved = 0;
+    recs[P.caller] = o;
+  }
+}
+
+extern "C" void* bg_export_kernel_ptr() { return (void*)&bg_export_kernel; }
+
 // ------------------------------------------------------------------ instantiation table
 
 typedef void (*bg_dp_fn)(BgDpArgs);

@@ -135,6 +135,18 @@ typedef struct bg_stats {
 
 int bg_get_stats(bg_aligner* h, bg_stats* out);
 
+/* Kernel timing over a region of executes (HIP events recorded on the handle's stream around
+ * the DP and the finish kernel of every execute; up to 4096 executes per region).
+ * bg_profile_end waits for the work and returns per-execute averages in milliseconds. */
+int bg_profile_begin(bg_aligner* h);
+int bg_profile_end(bg_aligner* h, float* avg_dp_ms, float* avg_finish_ms, int* executes);
+
+/* Device-to-device export of the last execute's results for a collective (e.g. an RCCL
+ * gather to rank 0): dst (device memory, same GPU) receives the packed record
+ *   [u64 npairs][bg_pair_result x npairs][aligned1 bytes][aligned2 bytes]
+ * with offsets as in bg_batch_fetch.  Pass dst = NULL to query the size in *bytes. */
+int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes);
+
 /* Tuning overrides for tests/benchmarks (0 = automatic). */
 int bg_set_tuning(bg_aligner* h, int R, int waves);
 
