@@ -75,6 +75,8 @@ def main():
     ap.add_argument("--extend", type=int, default=-2)
     ap.add_argument("--R", type=int, default=0)
     ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="2: traceback of step k overlaps the DP of step k+1 (two HIP streams)")
     ap.add_argument("--cpu-pairs", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
@@ -95,6 +97,7 @@ def main():
     h = _native.Handle(local_rank)
     if args.R or args.waves:
         h.set_tuning(args.R, args.waves)
+    h.set_pipeline(args.pipeline)
     pairs = make_pairs(args.pairs, args.len1, args.len2, SEED + 1000003 * rank)
     sc = _native.builtin_scoring(_native.BG_BLOSUM62)
     h.prepare(args.mode, pairs, sc, args.open, args.extend)
@@ -200,7 +203,7 @@ def main():
                    "len2": args.len2, "mode": args.mode, "scoring": "blosum62",
                    "gap_open": args.open, "gap_extend": args.extend,
                    "kernel": {"R": st["R"], "waves": st["waves"], "affine": st["affine"],
-                              "dna_profile": st["dna"]},
+                              "dna_profile": st["dna"], "pipeline": args.pipeline},
                    "parallelism": "dp%d (independent pairs per rank)" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

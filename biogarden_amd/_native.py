@@ -19,7 +19,8 @@ BG_BLOSUM62, BG_PAM250, BG_UNIT = range(3)
 EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align",
            "bg_align_batch", "bg_batch_prepare", "bg_batch_execute", "bg_batch_fetch",
            "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
-           "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export"]
+           "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
+           "bg_set_pipeline"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -85,6 +86,7 @@ def lib():
                                  ctypes.c_size_t]
     L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
     L.bg_set_tuning.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    L.bg_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.bg_status_string.argtypes = [ctypes.c_int]
     L.bg_status_string.restype = ctypes.c_char_p
     L.bg_abi_version.restype = ctypes.c_int
@@ -129,6 +131,9 @@ class Handle:
 
     def set_tuning(self, R=0, waves=0):
         check(lib().bg_set_tuning(self._p, R, waves))
+
+    def set_pipeline(self, depth):
+        check(lib().bg_set_pipeline(self._p, depth))
 
     @staticmethod
     def _arrays(pairs):

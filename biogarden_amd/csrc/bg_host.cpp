@@ -20,7 +20,8 @@
 #include "biogarden_gpu.h"
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
-extern "C" void* bg_finish_kernel_ptr();
+extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
+extern "C" size_t bg_finish_lds_bytes();
 extern "C" void* bg_export_kernel_ptr();
 
 #include "bg_tables.inc"
@@ -52,12 +53,25 @@ inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
 }  // namespace
 
+// Per-execute arenas.  Two slots let the finish kernel of execute k (stream2) run while the
+// DP kernel of execute k+1 (stream) fills the other slot's trace.
+struct Slot {
+  DevBuf trace, bndM, bndX, aux, out1, out2, results;
+  hipEvent_t dpDone = nullptr, finDone = nullptr;
+  bool inflight = false;
+};
+
 struct bg_aligner {
   int device = 0;
   int cus = 256;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-  DevBuf seq1, seq2, lut, prof, pairs, trace, bndM, bndX, aux, out1, out2, results, recs;
+  hipStream_t stream = nullptr;    // uploads, DP kernels, downloads
+  hipStream_t stream2 = nullptr;   // end cell + traceback kernels
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
+  DevBuf seq1, seq2, lut, prof, pairs, recs;
+  Slot slot[2];
+  int depth = 2;                   // pipeline depth (1 or 2 slots)
+  int execCount = 0;
+  int lastSlot = 0;
 
   // profiling ring (bg_profile_begin/end)
   std::vector<hipEvent_t> ring;
@@ -80,13 +94,16 @@ struct bg_aligner {
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
   float dp_ms = 0.f, fin_ms = 0.f;
+  hipEvent_t last[4] = {nullptr, nullptr, nullptr, nullptr};
 
   std::vector<BgResult> hres;
   std::vector<uint8_t> ho1, ho2;
 
   size_t device_bytes() const {
-    return seq1.cap + seq2.cap + lut.cap + prof.cap + pairs.cap + trace.cap + bndM.cap +
-           bndX.cap + aux.cap + out1.cap + out2.cap + results.cap + recs.cap;
+    size_t t = seq1.cap + seq2.cap + lut.cap + prof.cap + pairs.cap + recs.cap;
+    for (const Slot& S : slot)
+      t += S.trace.cap + S.bndM.cap + S.bndX.cap + S.aux.cap + S.out1.cap + S.out2.cap + S.results.cap;
+    return t;
   }
 };
 
@@ -138,9 +155,19 @@ extern "C" bg_aligner* bg_aligner_new(int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     h->cus = prop.multiProcessorCount;
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) { delete h; return nullptr; }
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess) {
+    bg_aligner_free(h);
+    return nullptr;
+  }
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) { bg_aligner_free(h); return nullptr; }
+  for (Slot& S : h->slot)
+    if (hipEventCreateWithFlags(&S.dpDone, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.finDone, hipEventDisableTiming) != hipSuccess) {
+      bg_aligner_free(h);
+      return nullptr;
+    }
   return h;
 }
 
@@ -148,14 +175,19 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
-  for (DevBuf* d : {&h->seq1, &h->seq2, &h->lut, &h->prof, &h->pairs, &h->trace, &h->bndM, &h->bndX,
-                    &h->aux, &h->out1, &h->out2, &h->results, &h->recs})
-    d->release();
+  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+  for (DevBuf* d : {&h->seq1, &h->seq2, &h->lut, &h->prof, &h->pairs, &h->recs}) d->release();
+  for (Slot& S : h->slot) {
+    for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results}) d->release();
+    if (S.dpDone) (void)hipEventDestroy(S.dpDone);
+    if (S.finDone) (void)hipEventDestroy(S.finDone);
+  }
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
   for (auto& e : h->ring)
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->stream2) (void)hipStreamDestroy(h->stream2);
   delete h;
 }
 
@@ -163,6 +195,17 @@ extern "C" int bg_set_tuning(bg_aligner* h, int R, int waves) {
   if (!h || (R != 0 && R != 4 && R != 8) || waves < 0 || waves > 16) return BG_E_ARG;
   h->tuneR = R;
   h->tuneW = waves;
+  return BG_OK;
+}
+
+extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
+  if (!h || depth < 1 || depth > 2) return BG_E_ARG;
+  if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
+      hipStreamSynchronize(h->stream2) != hipSuccess)
+    return BG_E_HIP;
+  h->depth = depth;
+  h->prepared = false;   // arenas are sized at prepare time
+  h->executed = false;
   return BG_OK;
 }
 
@@ -178,6 +221,10 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   if (npairs && (!s1 || !n1 || !s2 || !n2)) return BG_E_ARG;
   if (sc->alphabet_size < 0 || sc->alphabet_size > 32) return BG_E_ARG;
   BG_HIP(hipSetDevice(h->device));
+  BG_HIP(hipStreamSynchronize(h->stream));
+  BG_HIP(hipStreamSynchronize(h->stream2));
+  for (Slot& S : h->slot) S.inflight = false;
+  h->execCount = 0;
   h->prepared = false;
   h->executed = false;
   h->mode = mode;
@@ -321,12 +368,16 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
 
   // ---- device memory
   if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->lut.ensure(256) ||
-      !h->prof.ensure(2048) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
-      !h->trace.ensure(tro + 256) || !h->bndM.ensure(bo * 4 + 256) ||
-      !h->bndX.ensure(h->affine ? bo * 4 + 256 : 256) || !h->aux.ensure(ao * 4 + 256) ||
-      !h->out1.ensure(oo + 16) || !h->out2.ensure(oo + 16) ||
-      !h->results.ensure(sizeof(BgResult) * (h->plan.size() + 1)))
+      !h->prof.ensure(2048) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)))
     return BG_E_NOMEM;
+  for (int z = 0; z < h->depth; ++z) {
+    Slot& S = h->slot[z];
+    if (!S.trace.ensure(tro + 256) || !S.bndM.ensure(bo * 4 + 256) ||
+        !S.bndX.ensure(h->affine ? bo * 4 + 256 : 256) || !S.aux.ensure(ao * 4 + 256) ||
+        !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) ||
+        !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)))
+      return BG_E_NOMEM;
+  }
 
   // ---- uploads
   std::vector<uint8_t> st1(o1 + 1), st2(o2 + 1);
@@ -389,14 +440,16 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   if (!h->prepared) return BG_E_NO_BATCH;
   BG_HIP(hipSetDevice(h->device));
   const unsigned np = (unsigned)h->plan.size();
-  hipEvent_t e0 = h->ev[0], e1 = h->ev[1], e2 = h->ev[2];
-  if (h->profiling && h->ringUsed + 3 <= (int)h->ring.size()) {
-    e0 = h->ring[h->ringUsed];
-    e1 = h->ring[h->ringUsed + 1];
-    e2 = h->ring[h->ringUsed + 2];
-    h->ringUsed += 3;
+  const int z = h->execCount % h->depth;
+  Slot& S = h->slot[z];
+  // the previous user of this slot must have finished reading its trace
+  if (S.inflight) BG_HIP(hipStreamWaitEvent(h->stream, S.finDone, 0));
+  hipEvent_t e[4] = {h->ev[0], h->ev[1], h->ev[2], h->ev[3]};
+  if (h->profiling && h->ringUsed + 4 <= (int)h->ring.size()) {
+    for (int x = 0; x < 4; ++x) e[x] = h->ring[h->ringUsed + x];
+    h->ringUsed += 4;
   }
-  BG_HIP(hipEventRecord(e0, h->stream));
+  BG_HIP(hipEventRecord(e[0], h->stream));
   if (np) {
     void* fn = bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
     if (!fn) return BG_E_ARG;
@@ -405,10 +458,10 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.seq1 = h->seq1.as<uint8_t>();
     A.seq2 = h->seq2.as<uint8_t>();
     A.lut = h->lut.as<uint8_t>();
-    A.trace = h->trace.as<uint32_t>();
-    A.bndM = h->bndM.as<int32_t>();
-    A.bndX = h->bndX.as<int32_t>();
-    A.aux = h->aux.as<int32_t>();
+    A.trace = S.trace.as<uint32_t>();
+    A.bndM = S.bndM.as<int32_t>();
+    A.bndX = S.bndX.as<int32_t>();
+    A.aux = S.aux.as<int32_t>();
     A.profile = h->prof.as<int32_t>();
     A.kdim = h->kdim;
     A.open = h->a;
@@ -416,20 +469,25 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.mode = h->mode;
     A.npairs = (int32_t)np;
     void* args[] = {&A};
+    if (h->lds > 65536)
+      BG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds));
     BG_HIP(hipLaunchKernel(fn, dim3(np), dim3(64 * h->W), args, h->lds, h->stream));
   }
-  BG_HIP(hipEventRecord(e1, h->stream));
+  BG_HIP(hipEventRecord(e[1], h->stream));
+  BG_HIP(hipEventRecord(S.dpDone, h->stream));
+  BG_HIP(hipStreamWaitEvent(h->stream2, S.dpDone, 0));
+  BG_HIP(hipEventRecord(e[2], h->stream2));
   if (np) {
     BgFinishArgs F;
     F.pairs = h->pairs.as<BgPair>();
     F.seq1 = h->seq1.as<uint8_t>();
     F.seq2 = h->seq2.as<uint8_t>();
-    F.trace = h->trace.as<uint32_t>();
-    F.bndM = h->bndM.as<int32_t>();
-    F.aux = h->aux.as<int32_t>();
-    F.out1 = h->out1.as<uint8_t>();
-    F.out2 = h->out2.as<uint8_t>();
-    F.results = h->results.as<BgResult>();
+    F.trace = S.trace.as<uint32_t>();
+    F.bndM = S.bndM.as<int32_t>();
+    F.aux = S.aux.as<int32_t>();
+    F.out1 = S.out1.as<uint8_t>();
+    F.out2 = S.out2.as<uint8_t>();
+    F.results = S.results.as<BgResult>();
     F.open = h->a;
     F.ext = h->b;
     F.mode = h->mode;
@@ -437,12 +495,19 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.affine = h->affine;
     F.npairs = (int32_t)np;
     void* args[] = {&F};
-    BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(), dim3(np), dim3(64), args, 0, h->stream));
+    BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(h->R, h->affine, h->mode), dim3(np), dim3(256), args,
+                           bg_finish_lds_bytes(), h->stream2));
   }
-  BG_HIP(hipEventRecord(e2, h->stream));
-  if (e0 != h->ev[0]) {  // keep ev[] meaning "last execute" for bg_get_stats
-    h->ev[0] = e0; h->ev[1] = e1; h->ev[2] = e2;
+  BG_HIP(hipEventRecord(e[3], h->stream2));
+  BG_HIP(hipEventRecord(S.finDone, h->stream2));
+  S.inflight = true;
+  if (e[0] != h->ev[0]) {  // keep the last execute's events for bg_get_stats
+    h->last[0] = e[0]; h->last[1] = e[1]; h->last[2] = e[2]; h->last[3] = e[3];
+  } else {
+    for (int x = 0; x < 4; ++x) h->last[x] = h->ev[x];
   }
+  h->lastSlot = z;
+  ++h->execCount;
   h->executed = true;
   return BG_OK;
 }
@@ -451,9 +516,10 @@ extern "C" int bg_synchronize(bg_aligner* h) {
   if (!h) return BG_E_ARG;
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream));
+  BG_HIP(hipStreamSynchronize(h->stream2));
   if (h->executed) {
-    (void)hipEventElapsedTime(&h->dp_ms, h->ev[0], h->ev[1]);
-    (void)hipEventElapsedTime(&h->fin_ms, h->ev[1], h->ev[2]);
+    (void)hipEventElapsedTime(&h->dp_ms, h->last[0], h->last[1]);
+    (void)hipEventElapsedTime(&h->fin_ms, h->last[2], h->last[3]);
   }
   return BG_OK;
 }
@@ -472,9 +538,10 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   h->ho1.resize(ob + 1);
   h->ho2.resize(ob + 1);
   if (np) {
-    BG_HIP(hipMemcpyAsync(h->hres.data(), h->results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, h->stream));
-    BG_HIP(hipMemcpyAsync(h->ho1.data(), h->out1.p, ob, hipMemcpyDeviceToHost, h->stream));
-    BG_HIP(hipMemcpyAsync(h->ho2.data(), h->out2.p, ob, hipMemcpyDeviceToHost, h->stream));
+    const Slot& S = h->slot[h->lastSlot];
+    BG_HIP(hipMemcpyAsync(h->hres.data(), S.results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, h->stream));
+    BG_HIP(hipMemcpyAsync(h->ho1.data(), S.out1.p, ob, hipMemcpyDeviceToHost, h->stream));
+    BG_HIP(hipMemcpyAsync(h->ho2.data(), S.out2.p, ob, hipMemcpyDeviceToHost, h->stream));
     BG_HIP(hipStreamSynchronize(h->stream));
   }
   for (size_t p = 0; p < h->npairs; ++p) {
@@ -551,7 +618,7 @@ extern "C" int bg_profile_begin(bg_aligner* h) {
   if (!h) return BG_E_ARG;
   BG_HIP(hipSetDevice(h->device));
   if (h->ring.empty()) {
-    h->ring.resize(3 * 4096 + 3, nullptr);
+    h->ring.resize(4 * 4096, nullptr);
     for (auto& e : h->ring) BG_HIP(hipEventCreate(&e));
   }
   h->profiling = true;
@@ -563,12 +630,13 @@ extern "C" int bg_profile_end(bg_aligner* h, float* avg_dp, float* avg_fin, int*
   if (!h) return BG_E_ARG;
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream));
+  BG_HIP(hipStreamSynchronize(h->stream2));
   double dp = 0, fin = 0;
-  const int cnt = h->ringUsed / 3;
+  const int cnt = h->ringUsed / 4;
   for (int i = 0; i < cnt; ++i) {
     float x = 0, y = 0;
-    BG_HIP(hipEventElapsedTime(&x, h->ring[3 * i], h->ring[3 * i + 1]));
-    BG_HIP(hipEventElapsedTime(&y, h->ring[3 * i + 1], h->ring[3 * i + 2]));
+    BG_HIP(hipEventElapsedTime(&x, h->ring[4 * i], h->ring[4 * i + 1]));
+    BG_HIP(hipEventElapsedTime(&y, h->ring[4 * i + 2], h->ring[4 * i + 3]));
     dp += x;
     fin += y;
   }
@@ -587,6 +655,8 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   if (*bytes < need) return BG_E_ARG;
   if (!h->executed) return BG_E_NO_BATCH;
   BG_HIP(hipSetDevice(h->device));
+  BG_HIP(hipStreamSynchronize(h->stream2));
+  const Slot& S = h->slot[h->lastSlot];
   const uint64_t n = h->npairs;
   BG_HIP(hipMemcpyAsync(dst, &n, 8, hipMemcpyHostToDevice, h->stream));
   if (n)
@@ -595,9 +665,9 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   if (!h->plan.empty()) {
     BgExportArgs E;
     E.pairs = h->pairs.as<BgPair>();
-    E.results = h->results.as<BgResult>();
-    E.out1 = h->out1.as<uint8_t>();
-    E.out2 = h->out2.as<uint8_t>();
+    E.results = S.results.as<BgResult>();
+    E.out1 = S.out1.as<uint8_t>();
+    E.out2 = S.out2.as<uint8_t>();
     E.dst = (uint8_t*)dst;
     E.npairs_caller = n;
     E.out_bytes = h->outBytes;

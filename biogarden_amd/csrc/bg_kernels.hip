@@ -242,16 +242,16 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
     }
 
   }
-  // ---- trace flush every 32 steps: R*NW coalesced 256-B stores
+  // ---- trace flush every 32 steps: R coalesced stores of NW words per lane
+  //      layout: block b, row k, lane r -> dwords [((b*R + k)*64 + r)*NW, +NW)
   {
-    uint32_t* tb = C.trace + (size_t)((t0 >> 5) + h) * (R * NW * BG_WAVE) + lane;
+    uint32_t* tb = C.trace + (size_t)((t0 >> 5) + h) * (R * NW * BG_WAVE) + lane * NW;
 #pragma unroll
     for (int k = 0; k < R; ++k) {
-      tb[(k * NW + 0) * BG_WAVE] = S.tA[k];
-      tb[(k * NW + 1) * BG_WAVE] = S.tB[k];
       if constexpr (AFFINE) {
-        tb[(k * NW + 2) * BG_WAVE] = S.tC[k];
-        tb[(k * NW + 3) * BG_WAVE] = S.tD[k];
+        *reinterpret_cast<uint4*>(tb + k * NW * BG_WAVE) = make_uint4(S.tA[k], S.tB[k], S.tC[k], S.tD[k]);
+      } else {
+        *reinterpret_cast<uint2*>(tb + k * NW * BG_WAVE) = make_uint2(S.tA[k], S.tB[k]);
       }
     }
   }
@@ -438,158 +438,280 @@ __device__ __forceinline__ int unbias(unsigned v) { return (int)(v ^ 0x80000000u
 
 }  // namespace
 
-__global__ __launch_bounds__(64) void bg_finish_kernel(BgFinishArgs F) {
+// Trace-window geometry of the finish kernel: a window of 32-step trace blocks of one strip
+// staged in LDS, plus an 8x8 neighbourhood of decoded cells held one per lane.
+constexpr int kWinBytes = 57344;  // 56 KiB window + scalars/scan, under the 64 KiB default
+constexpr int kCodeMiss = 32, kCodeBorder = 16;
+
+template <int R, bool AFFINE, int MODE>
+__global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int NW = AFFINE ? 4 : 2;
+  constexpr int LOGR = (R == 4) ? 2 : 3;
+  constexpr int LOGROWS = 6 + LOGR;
+  constexpr int BLK_DW = R * BG_WAVE * NW;             // dwords per 32-step trace block
+  constexpr int NBW = kWinBytes / (BLK_DW * 4);        // blocks per window
+  uint32_t* win = reinterpret_cast<uint32_t*>(smem);
+  int* sh = reinterpret_cast<int*>(smem + kWinBytes);  // 64 ints of block-shared scalars
+  int* scan = sh + 64;                                 // 2 x 256 ints
+
   const BgPair& P = F.pairs[blockIdx.x];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6), NT = blockDim.x;
   Fin f;
   f.F = &F; f.P = &P;
   f.n1 = P.n1; f.n2 = P.n2; f.a = F.open; f.b = F.ext; f.mode = F.mode;
   f.s1 = F.seq1 + P.off1;
   f.s2 = F.seq2 + P.off2;
-  const int R = F.R;
-  const int NW = F.affine ? 4 : 2;
   f.lastrowMa = (P.nstrips > 0) ? F.bndM + P.bnd_off + (size_t)(P.nstrips - 1) * P.nc * BG_CHUNK : nullptr;
   f.lastcol = F.aux + P.aux_off;
   const int n1 = f.n1, n2 = f.n2;
+  constexpr int mode = MODE;
+  const int cap = n1 + n2;
+  uint8_t* ob = F.out1 + P.out_off;                    // op codes, then aligned seq1 (in place)
+  uint8_t* ob2 = F.out2 + P.out_off;
 
-  // ---------------- end cell (aligner.rs:112, 173-176, 247-251, 308-312, 369-389)
-  int ei = n1, ej = n2, score = 0, colcase = 0;
-  if (f.mode == BGK_GLOBAL) {
-    score = lastcolM(f, n1);
-  } else if (f.mode == BGK_LOCAL) {
-    // first row-major cell with the strict maximum; (0,0) with 0 when nothing is positive
-    u64 key = 0;
-    const int32_t* rowbest = f.lastcol + (n1 + 1);
-    const int32_t* rowpos = rowbest + n1;
-    if (n2 > 0)
-      for (int i = 1 + lane; i <= n1; i += 64) {
-        const u64 kk = ((u64)bias(rowbest[i - 1]) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+  // ---------------- end cell (aligner.rs:112, 173-176, 247-251, 308-312, 369-389): wave 0
+  if (wid == 0) {
+    int ei = n1, ej = n2, score = 0, colcase = 0;
+    if (mode == BGK_GLOBAL) {
+      score = lastcolM(f, n1);
+    } else if (mode == BGK_LOCAL) {
+      // first row-major cell with the strict maximum; (0,0) with 0 when nothing is positive
+      u64 key = 0;
+      const int32_t* rowbest = f.lastcol + (n1 + 1);
+      const int32_t* rowpos = rowbest + n1;
+      if (n2 > 0)
+        for (int i = 1 + lane; i <= n1; i += 64) {
+          const u64 kk = ((u64)bias(rowbest[i - 1]) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+          key = kk > key ? kk : key;
+        }
+      key = wave_max_u64(key);
+      const int v = unbias((unsigned)(key >> 32));
+      if (key != 0 && v > 0) {
+        ei = (int)(0xFFFFFFFFu - (unsigned)key);
+        ej = rowpos[ei - 1];
+        score = v;
+      } else {
+        ei = 0; ej = 0; score = 0;
+      }
+    } else if (mode == BGK_FITTING) {
+      u64 key = 0;                                   // first i, strict > (:247-249)
+      for (int i = lane; i <= n1; i += 64) {
+        const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
         key = kk > key ? kk : key;
       }
-    key = wave_max_u64(key);
-    const int v = unbias((unsigned)(key >> 32));
-    if (key != 0 && v > 0) {
-      ei = (int)(0xFFFFFFFFu - (unsigned)key);
-      ej = rowpos[ei - 1];
-      score = v;
-    } else {
-      ei = 0; ej = 0; score = 0;
-    }
-  } else if (f.mode == BGK_FITTING) {
-    u64 key = 0;                                   // first i, strict > (:247-249)
-    for (int i = lane; i <= n1; i += 64) {
-      const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
-      key = kk > key ? kk : key;
-    }
-    key = wave_max_u64(key);
-    ei = (int)(0xFFFFFFFFu - (unsigned)key); ej = n2; score = unbias((unsigned)(key >> 32));
-  } else if (f.mode == BGK_OVERLAP) {
-    u64 key = 0;                                   // last j, >= (:308-310)
-    for (int j = lane; j <= n2; j += 64) {
-      const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
-      key = kk > key ? kk : key;
-    }
-    key = wave_max_u64(key);
-    ei = n1; ej = (int)(unsigned)key; score = unbias((unsigned)(key >> 32));
-  } else {
-    u64 kr = 0, kc = 0;
-    for (int j = lane; j <= n2; j += 64) {         // last row, >= (:369-371)
-      const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
-      kr = kk > kr ? kk : kr;
-    }
-    for (int i = lane; i <= n1; i += 64) {         // last column, > (:376-378)
-      const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
-      kc = kk > kc ? kk : kc;
-    }
-    kr = wave_max_u64(kr);
-    kc = wave_max_u64(kc);
-    const int mr = unbias((unsigned)(kr >> 32)), mc = unbias((unsigned)(kc >> 32));
-    colcase = mc > mr;                             // (:389)
-    if (colcase) { ei = (int)(0xFFFFFFFFu - (unsigned)kc); ej = n2; score = mc; }
-    else { ei = n1; ej = (int)(unsigned)kr; score = mr; }
-  }
-  if (lane != 0) return;
-
-  // ---------------- traceback (aligner.rs:511-592), written backwards into the pair's slot
-  uint8_t* o1 = F.out1 + P.out_off;
-  uint8_t* o2 = F.out2 + P.out_off;
-  int pos = n1 + n2;
-  int status = 0;
-  auto emit = [&](uint8_t c1, uint8_t c2) { --pos; o1[pos] = c1; o2[pos] = c2; };
-  int k = ei, l = ej;
-  if (f.mode == BGK_SEMIGLOBAL) {                  // tail gaps (:389-404)
-    if (colcase) for (int i = n1; i >= ei + 1; --i) emit(f.s1[i - 1], '-');
-    else for (int j = n2; j >= ej + 1; --j) emit('-', f.s2[j - 1]);
-  }
-  const uint32_t* tr = F.trace + P.trace_off / 4;
-  const int ROWS = 64 * R;
-  const size_t stripDw = (size_t)P.nc * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE;
-  // trace bits of interior cell (k,l): bit0 = m0, bit1 = m1, bit2 = x_trace=='M', bit3 = y_trace=='M'
-  auto fetch = [&](int kk, int ll) -> int {
-    const int vr = kk - 1;
-    const int sidx = vr / ROWS, rem = vr % ROWS, r = rem / R, q = rem % R;
-    const int t = ll + r;
-    const size_t base = (size_t)sidx * stripDw + ((size_t)(t >> 5) * R + q) * NW * BG_WAVE + r;
-    const int bit = 31 - (t & 31);
-    int v = ((tr[base] >> bit) & 1) | (((tr[base + BG_WAVE] >> bit) & 1) << 1);
-    if (F.affine) v |= (((tr[base + 2 * BG_WAVE] >> bit) & 1) << 2) | (((tr[base + 3 * BG_WAVE] >> bit) & 1) << 3);
-    else v |= 12;
-    return v;
-  };
-  int state = 0;  // 0 = M, 1 = X, 2 = Y
-  for (;;) {
-    // trace_valid (:117, :181, :256, :317, :409)
-    bool ok;
-    int bits = 0;
-    const bool interior = k > 0 && l > 0;
-    if (interior) bits = fetch(k, l);
-    if (f.mode == BGK_GLOBAL) ok = (k != 0 || l != 0);
-    else if (f.mode == BGK_LOCAL) ok = interior && (bits & 3) != 3;
-    else if (f.mode == BGK_SEMIGLOBAL) ok = interior;
-    else ok = l != 0;
-    if (!ok) break;
-    if (state == 0) {
-      // m_trace: borders column 0 = 'X', row 0 = 'Y' (row fill last, so (0,0) = 'Y')
-      int mt;  // 0 R, 1 X, 2 Y
-      if (!interior) mt = (k == 0) ? 2 : 1;
-      else mt = (bits & 1) ? 2 : ((bits & 2) ? 1 : 0);
-      if (mt == 0) {
-        if (k == 0 || l == 0) { status = 4; break; }
-        emit(f.s1[k - 1], f.s2[l - 1]); --k; --l;
-      } else if (mt == 1) {
-        state = 1;
-        if (k == 0) { status = 4; break; }
-        emit(f.s1[k - 1], '-'); --k;
-      } else {
-        state = 2;
-        if (l == 0) { status = 4; break; }
-        emit('-', f.s2[l - 1]); --l;
+      key = wave_max_u64(key);
+      ei = (int)(0xFFFFFFFFu - (unsigned)key); ej = n2; score = unbias((unsigned)(key >> 32));
+    } else if (mode == BGK_OVERLAP) {
+      u64 key = 0;                                   // last j, >= (:308-310)
+      for (int j = lane; j <= n2; j += 64) {
+        const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
+        key = kk > key ? kk : key;
       }
-    } else if (state == 1) {
-      const bool toM = interior && (bits & 4);      // x_trace border = 'I'
-      if (toM) state = 0;
-      else { if (k == 0) { status = 4; break; } emit(f.s1[k - 1], '-'); --k; }
+      key = wave_max_u64(key);
+      ei = n1; ej = (int)(unsigned)key; score = unbias((unsigned)(key >> 32));
     } else {
-      const bool toM = interior && (bits & 8);
-      if (toM) state = 0;
-      else { if (l == 0) { status = 4; break; } emit('-', f.s2[l - 1]); --l; }
+      u64 kr = 0, kc = 0;
+      for (int j = lane; j <= n2; j += 64) {         // last row, >= (:369-371)
+        const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
+        kr = kk > kr ? kk : kr;
+      }
+      for (int i = lane; i <= n1; i += 64) {         // last column, > (:376-378)
+        const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+        kc = kk > kc ? kk : kc;
+      }
+      kr = wave_max_u64(kr);
+      kc = wave_max_u64(kc);
+      const int mr = unbias((unsigned)(kr >> 32)), mc = unbias((unsigned)(kc >> 32));
+      colcase = mc > mr;                             // (:389)
+      if (colcase) { ei = (int)(0xFFFFFFFFu - (unsigned)kc); ej = n2; score = mc; }
+      else { ei = n1; ej = (int)(unsigned)kr; score = mr; }
     }
+    if (lane == 0) { sh[0] = ei; sh[1] = ej; sh[2] = score; sh[3] = colcase; }
   }
-  const int start1 = k, start2 = l;                  // where the walk stopped
-  if (status == 0 && f.mode == BGK_SEMIGLOBAL) {    // prefix gaps (:416-428)
-    if (colcase) for (int i = k; i >= 1; --i) emit(f.s1[i - 1], '-');
-    else for (int j = l; j >= 1; --j) emit('-', f.s2[j - 1]);
+  __syncthreads();
+  const int ei = uni(sh[0]), ej = uni(sh[1]), score = uni(sh[2]), colcase = uni(sh[3]);
+
+  // ---------------- semiglobal tail gaps (:389-404): ops written backwards from the slot end
+  // op codes: 0 = (s1, s2), 1 = (s1, '-'), 2 = ('-', s2)
+  const int ntail = (mode == BGK_SEMIGLOBAL) ? (colcase ? n1 - ei : n2 - ej) : 0;
+  for (int x = tid; x < ntail; x += NT) ob[cap - 1 - x] = colcase ? 1 : 2;
+
+  // ---------------- traceback walk (aligner.rs:511-592)
+  const uint32_t* tr = F.trace + P.trace_off / 4;
+  const size_t stripDw = (size_t)P.nc * (BG_CHUNK / BG_TRACE_BLK) * BLK_DW;
+  const int stripBlocks = P.nc * (BG_CHUNK / BG_TRACE_BLK);
+  int k = ei, l = ej, state = 0, status = 0, ncore = 0;
+  int curS = -1, curB0 = 0, curNb = 0;
+  int k0 = -1000000, l0 = -1000000;                  // neighbourhood anchor (invalid)
+  int codes = 0, opacc = 0;
+  // Transition table of backtrack (aligner.rs:520-586), per state, indexed by the 4-bit cell code
+  // (bits 0-1 m_trace: 0 'R', 1 'X', 2 'Y', 3 STOP; bit 2 x_trace=='M'; bit 3 y_trace=='M').
+  // Entry = (move << 2) | next state; move 0 none, 1 diag (op 0), 2 up (op 1), 3 left (op 2).
+  constexpr u64 kLutM = [] {
+    u64 v = 0;
+    for (int c = 0; c < 16; ++c) {
+      const int mt = c & 3;
+      const u64 e = mt == 0 ? (1u << 2) | 0 : mt == 1 ? (2u << 2) | 1 : mt == 2 ? (3u << 2) | 2 : 0;
+      v |= e << (4 * c);
+    }
+    return v;
+  }();
+  constexpr u64 kLutX = [] {
+    u64 v = 0;
+    for (int c = 0; c < 16; ++c) v |= (u64)((c & 4) ? 0 : ((2u << 2) | 1)) << (4 * c);
+    return v;
+  }();
+  constexpr u64 kLutY = [] {
+    u64 v = 0;
+    for (int c = 0; c < 16; ++c) v |= (u64)((c & 8) ? 0 : ((3u << 2) | 2)) << (4 * c);
+    return v;
+  }();
+  for (;;) {
+    int reqS = -1, reqB0 = 0, done = 0;
+    if (wid == 0) {
+      for (;;) {
+        int dk = k0 - k, dl = l0 - l;
+        if ((unsigned)dk >= 8u || (unsigned)dl >= 8u) {
+          // re-anchor: lane (dk, dl) decodes cell (k - dk, l - dl)
+          k0 = k; l0 = l; dk = 0; dl = 0;
+          const int kk = k0 - (lane >> 3), ll = l0 - (lane & 7);
+          if (kk <= 0 || ll <= 0) {
+            codes = kCodeBorder | ((kk == 0) ? 2 : 1);  // m_trace borders: column 0 'X', row 0 'Y'
+          } else {
+            const int vr = kk - 1;
+            const int sidx = vr >> LOGROWS, r = (vr >> LOGR) & 63, q = vr & (R - 1);
+            const int t = ll + r, bl = t >> 5;
+            if (sidx != curS || bl < curB0 || bl >= curB0 + curNb) {
+              codes = kCodeMiss;
+            } else {
+              const uint32_t* wp = win + (((bl - curB0) * R + q) * BG_WAVE + r) * NW;
+              const int bit = 31 - (t & 31);
+              int c;
+              if constexpr (AFFINE) {
+                const uint4 v = *reinterpret_cast<const uint4*>(wp);
+                c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | (((v.z >> bit) & 1) << 2) | (((v.w >> bit) & 1) << 3);
+              } else {
+                const uint2 v = *reinterpret_cast<const uint2*>(wp);
+                c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | 12;
+              }
+              codes = c;
+            }
+          }
+        }
+        const int c = rdlane(codes, dk * 8 + dl);
+        if (c & kCodeMiss) {
+          const int vr = k - 1;
+          reqS = vr >> LOGROWS;
+          const int bl = (l + ((vr >> LOGR) & 63)) >> 5;
+          reqB0 = bl - NBW + 1 > 0 ? bl - NBW + 1 : 0;
+          break;
+        }
+        const bool interior = !(c & kCodeBorder);
+        bool ok;                                       // trace_valid (:117, :181, :256, :317, :409)
+        if constexpr (MODE == BGK_GLOBAL) ok = (k | l) != 0;
+        else if constexpr (MODE == BGK_LOCAL) ok = interior && (c & 3) != 3;
+        else if constexpr (MODE == BGK_SEMIGLOBAL) ok = interior;
+        else ok = l != 0;
+        if (!ok) { done = 1; break; }
+        const u64 lut = state == 0 ? kLutM : (state == 1 ? kLutX : kLutY);
+        const int e = (int)(lut >> (4 * (c & 15))) & 15;
+        const int mv = e >> 2;
+        if ((mv == 2 && k == 0) || (mv == 3 && l == 0)) { status = 4; done = 1; break; }  // index underflow panic
+        k -= (0x6 >> mv) & 1;
+        l -= (0xA >> mv) & 1;
+        state = e & 3;
+        if (mv) {
+          opacc = wrlane(mv - 1, ncore & 63, opacc);
+          if ((ncore & 63) == 63) ob[cap - 1 - (ntail + (ncore & ~63) + lane)] = (uint8_t)opacc;
+          ++ncore;
+        }
+      }
+      if (lane == 0) { sh[4] = reqS; sh[5] = reqB0; sh[6] = done; }
+    }
+    __syncthreads();
+    done = sh[6];
+    if (done) break;
+    reqS = uni(sh[4]);
+    reqB0 = uni(sh[5]);
+    {
+      const int nb = (stripBlocks - reqB0) < NBW ? (stripBlocks - reqB0) : NBW;
+      const uint4* src = reinterpret_cast<const uint4*>(tr + (size_t)reqS * stripDw + (size_t)reqB0 * BLK_DW);
+      uint4* dst = reinterpret_cast<uint4*>(win);
+      const int n4 = nb * BLK_DW / 4;
+      constexpr int UNR = 16;                            // all of a thread's loads in flight at once
+      for (int x0 = 0; x0 < n4; x0 += UNR * NT) {
+        uint4 v[UNR];
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const int x = x0 + u * NT + tid;
+          if (x < n4) v[u] = src[x];
+        }
+#pragma unroll
+        for (int u = 0; u < UNR; ++u) {
+          const int x = x0 + u * NT + tid;
+          if (x < n4) dst[x] = v[u];
+        }
+      }
+      curS = reqS; curB0 = reqB0; curNb = nb;
+      k0 = -1000000;                                   // decode the neighbourhood again
+    }
+    __syncthreads();
   }
-  BgResult res;
-  res.status = status;
-  res.score = score;
-  res.end_i = ei;
-  res.end_j = ej;
-  res.out_start = (uint32_t)pos;
-  res.out_len = (uint32_t)(n1 + n2 - pos);
-  res.start1 = (uint32_t)start1;
-  res.start2 = (uint32_t)start2;
-  F.results[P.index] = res;
+  if (wid == 0 && lane < (ncore & 63)) ob[cap - 1 - (ntail + (ncore & ~63) + lane)] = (uint8_t)opacc;
+
+  // ---------------- semiglobal prefix gaps (:416-428); every wave knows k, l through sh
+  if (wid == 0 && lane == 0) { sh[7] = k; sh[8] = l; sh[9] = status; sh[10] = ncore; }
+  __syncthreads();
+  const int kstop = sh[7], lstop = sh[8];
+  status = sh[9];
+  ncore = sh[10];
+  int npre = 0;
+  if (status == 0 && mode == BGK_SEMIGLOBAL) npre = colcase ? kstop : lstop;
+  for (int x = tid; x < npre; x += NT) ob[cap - 1 - (ntail + ncore + x)] = colcase ? 1 : 2;
+  const int L = ntail + ncore + npre;
+  __syncthreads();
+
+  // ---------------- expand ops into the two aligned strings (parallel scan over columns)
+  int i0 = kstop, j0 = lstop;                          // first residues the columns consume
+  if (mode == BGK_SEMIGLOBAL && status == 0) { if (colcase) i0 = 0; else j0 = 0; }
+  const int base = cap - L;
+  const int seg = (L + NT - 1) / NT;
+  const int lo = base + tid * seg < cap ? base + tid * seg : cap;
+  const int hi = lo + seg < cap ? lo + seg : cap;
+  int c1 = 0, c2 = 0;
+  for (int x = lo; x < hi; ++x) { const int op = ob[x]; c1 += op != 2; c2 += op != 1; }
+  scan[tid] = c1;
+  scan[NT + tid] = c2;
+  __syncthreads();
+  for (int o = 1; o < NT; o <<= 1) {                  // inclusive Hillis-Steele scan
+    const int v1 = tid >= o ? scan[tid - o] : 0;
+    const int v2 = tid >= o ? scan[NT + tid - o] : 0;
+    __syncthreads();
+    scan[tid] += v1;
+    scan[NT + tid] += v2;
+    __syncthreads();
+  }
+  int p1 = i0 + scan[tid] - c1, p2 = j0 + scan[NT + tid] - c2;
+  for (int x = lo; x < hi; ++x) {
+    const int op = ob[x];
+    const uint8_t ch1 = op != 2 ? f.s1[p1++] : (uint8_t)'-';
+    const uint8_t ch2 = op != 1 ? f.s2[p2++] : (uint8_t)'-';
+    ob[x] = ch1;
+    ob2[x] = ch2;
+  }
+  if (tid == 0) {
+    BgResult res;
+    res.status = status;
+    res.score = score;
+    res.end_i = ei;
+    res.end_j = ej;
+    res.out_start = (uint32_t)base;
+    res.out_len = (uint32_t)L;
+    res.start1 = (uint32_t)kstop;
+    res.start2 = (uint32_t)lstop;
+    F.results[P.index] = res;
+  }
 }
 
 // ------------------------------------------------------------------ export (for collectives)
@@ -662,4 +784,19 @@ extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna) {
   return nullptr;
 }
 
-extern "C" void* bg_finish_kernel_ptr() { return (void*)&bg_finish_kernel; }
+template <int R, bool AF>
+static void* finish_ptr(int mode) {
+  switch (mode) {
+    case BGK_GLOBAL: return (void*)&bg_finish_kernel<R, AF, BGK_GLOBAL>;
+    case BGK_LOCAL: return (void*)&bg_finish_kernel<R, AF, BGK_LOCAL>;
+    case BGK_FITTING: return (void*)&bg_finish_kernel<R, AF, BGK_FITTING>;
+    case BGK_OVERLAP: return (void*)&bg_finish_kernel<R, AF, BGK_OVERLAP>;
+    default: return (void*)&bg_finish_kernel<R, AF, BGK_SEMIGLOBAL>;
+  }
+}
+extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode) {
+  if (R == 4) return affine ? finish_ptr<4, true>(mode) : finish_ptr<4, false>(mode);
+  if (R == 8) return affine ? finish_ptr<8, true>(mode) : finish_ptr<8, false>(mode);
+  return nullptr;
+}
+extern "C" size_t bg_finish_lds_bytes() { return kWinBytes + 64 * 4 + 2 * 256 * 4; }

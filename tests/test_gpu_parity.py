@@ -241,3 +241,22 @@ def test_deterministic(aligner):
     r1 = aligner.align_batch("local", pairs, score.blosum62, -11, -1)
     r2 = aligner.align_batch("local", pairs, score.blosum62, -11, -1)
     assert [(x[0], x[1], x[2]) for x in r1] == [(x[0], x[1], x[2]) for x in r2]
+
+
+def test_pipelined_executes_match_single():
+    """Depth-2 pipeline (traceback of execute k overlapping DP of k+1) returns what a single
+    serialised execute returns."""
+    from biogarden_amd import _native
+    rng = random.Random(11)
+    pairs = [(rand_seq(rng, 2500, DNA), rand_seq(rng, 2200, DNA)) for _ in range(6)]
+    sc = _native.builtin_scoring(_native.BG_BLOSUM62)
+    h = _native.Handle(0)
+    h.set_pipeline(1)
+    want = h.align_batch("semiglobal", pairs, sc, -1, -2)
+    h.set_pipeline(2)
+    h.prepare("semiglobal", pairs, sc, -1, -2)
+    for _ in range(5):
+        h.execute()
+    got = h.fetch()
+    h.close()
+    assert got == want
