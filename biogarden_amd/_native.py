@@ -20,7 +20,7 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_align_batch", "bg_batch_prepare", "bg_batch_execute", "bg_batch_fetch",
            "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
            "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
-           "bg_set_pipeline"]
+           "bg_set_pipeline", "bg_set_kernel_options"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -44,7 +44,8 @@ class BgStats(ctypes.Structure):
     _fields_ = [("cells", ctypes.c_uint64), ("trace_bytes", ctypes.c_uint64),
                 ("boundary_bytes", ctypes.c_uint64), ("residue_bytes", ctypes.c_uint64),
                 ("device_bytes", ctypes.c_uint64), ("R", ctypes.c_int32),
-                ("waves", ctypes.c_int32), ("affine", ctypes.c_int32), ("dna", ctypes.c_int32),
+                ("waves", ctypes.c_int32), ("affine", ctypes.c_int32), ("tagged", ctypes.c_int32),
+                ("dna", ctypes.c_int32),
                 ("local", ctypes.c_int32), ("npairs", ctypes.c_int32),
                 ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float)]
 
@@ -87,6 +88,7 @@ def lib():
     L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
     L.bg_set_tuning.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     L.bg_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.bg_set_kernel_options.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.bg_status_string.argtypes = [ctypes.c_int]
     L.bg_status_string.restype = ctypes.c_char_p
     L.bg_abi_version.restype = ctypes.c_int
@@ -131,6 +133,9 @@ class Handle:
 
     def set_tuning(self, R=0, waves=0):
         check(lib().bg_set_tuning(self._p, R, waves))
+
+    def set_kernel_options(self, allow_tagged=True):
+        check(lib().bg_set_kernel_options(self._p, 1 if allow_tagged else 0))
 
     def set_pipeline(self, depth):
         check(lib().bg_set_pipeline(self._p, depth))

@@ -63,15 +63,21 @@ struct BgDpArgs {
   const uint8_t* seq1;     // raw bytes of seq1, all pairs
   const uint8_t* seq2;     // raw bytes of seq2, all pairs
   const uint8_t* lut;      // 256 entries: byte -> dense code (DNA path: code*8)
+  const uint8_t* codes1;   // lut[seq1] (host-computed), same offsets as seq1
+  const uint8_t* codes2;   // lut[seq2]
   uint32_t* trace;         // trace arena
   int32_t* bndM;           // strip-boundary rows: M + open, per strip output
   int32_t* bndX;           // strip-boundary rows: X (affine kernels only)
   int32_t* aux;            // lastcol / rowbest / rowpos
-  const int32_t* profile;  // DNA: [k] int32 = 4 packed int8 S(q=k, c) - open; LDS path: int16 [32][32]
+  const int32_t* profile;  // DNA: [q] = 4 packed int8 S(q, c) - open; tagged kernel: [64+q] packed
+                           // 4(S-open)-1, [128+q] packed 4(S-open)-2; LDS path: int16 [32][32]
   int32_t kdim;            // alphabet size (LDS path)
   int32_t open, ext;       // reference `a`, `b`
   int32_t mode;
   int32_t npairs;
+  int32_t prog_off;        // byte offset of the 16 per-wave progress counters in dynamic LDS
+  int32_t codes_off;       // byte offset of the staged seq2 codes in dynamic LDS
+  int32_t codes_in_lds;    // 1 if every pair's seq2 fits there
 };
 
 struct BgFinishArgs {
@@ -88,6 +94,7 @@ struct BgFinishArgs {
   int32_t mode;
   int32_t R;               // rows per lane of the DP kernel that produced the trace
   int32_t affine;          // trace carries x/y bits
+  int32_t tag;             // tagged linear kernel: 2-bit m_trace codes, boundary rows 4(M+a)+1
   int32_t npairs;
 };
 

@@ -20,6 +20,8 @@
 #include "biogarden_gpu.h"
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
+extern "C" int bg_dp_has_R(int R, int affine, int local, int dna);
+extern "C" void* bg_dp_kernel_tag_ptr(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes();
 extern "C" void* bg_export_kernel_ptr();
@@ -67,7 +69,7 @@ struct bg_aligner {
   hipStream_t stream = nullptr;    // uploads, DP kernels, downloads
   hipStream_t stream2 = nullptr;   // end cell + traceback kernels
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
-  DevBuf seq1, seq2, lut, prof, pairs, recs;
+  DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
   Slot slot[2];
   int depth = 2;                   // pipeline depth (1 or 2 slots)
   int execCount = 0;
@@ -89,8 +91,12 @@ struct bg_aligner {
   std::vector<uint64_t> outoff;      // caller output offsets
   std::vector<BgPair> plan;          // GPU pairs in launch (LPT) order
   std::vector<size_t> order_;        // plan slot -> caller index
-  int R = 8, W = 1, affine = 0, local = 0, dna = 1, kdim = 0;
+  int R = 8, W = 1, affine = 0, local = 0, dna = 1, kdim = 0, tag = 0;
+  int allowTag = 1;
   size_t lds = 0;
+  int progOff = 256;
+  int codesOff = 320;
+  int codesInLds = 0;
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
   float dp_ms = 0.f, fin_ms = 0.f;
@@ -100,7 +106,7 @@ struct bg_aligner {
   std::vector<uint8_t> ho1, ho2;
 
   size_t device_bytes() const {
-    size_t t = seq1.cap + seq2.cap + lut.cap + prof.cap + pairs.cap + recs.cap;
+    size_t t = seq1.cap + seq2.cap + codes1.cap + codes2.cap + lut.cap + prof.cap + pairs.cap + recs.cap;
     for (const Slot& S : slot)
       t += S.trace.cap + S.bndM.cap + S.bndX.cap + S.aux.cap + S.out1.cap + S.out2.cap + S.results.cap;
     return t;
@@ -176,7 +182,7 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
-  for (DevBuf* d : {&h->seq1, &h->seq2, &h->lut, &h->prof, &h->pairs, &h->recs}) d->release();
+  for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs}) d->release();
   for (Slot& S : h->slot) {
     for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results}) d->release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
@@ -192,9 +198,17 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
 }
 
 extern "C" int bg_set_tuning(bg_aligner* h, int R, int waves) {
-  if (!h || (R != 0 && R != 4 && R != 8) || waves < 0 || waves > 16) return BG_E_ARG;
+  if (!h || (R != 0 && R != 4 && R != 5 && R != 8 && R != 10) || waves < 0 || waves > 16) return BG_E_ARG;
   h->tuneR = R;
   h->tuneW = waves;
+  return BG_OK;
+}
+
+extern "C" int bg_set_kernel_options(bg_aligner* h, int allow_tagged) {
+  if (!h) return BG_E_ARG;
+  h->allowTag = allow_tagged ? 1 : 0;
+  h->prepared = false;
+  h->executed = false;
   return BG_OK;
 }
 
@@ -298,28 +312,65 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   const double bound = ((double)maxAbsS + std::abs((double)a) + std::abs((double)b)) *
                        ((double)maxn1 + (double)maxn2 + 2.0);
   h->affine = (a >= b && bound < 1073741824.0) ? 0 : 1;
+  // tagged linear kernel: values 4(M+a)+tag must stay far from overflow, 4(S-a)-1/-2 fit int8
+  bool tagOK = h->allowTag && !h->affine && mode != BG_LOCAL && dnaOK && bound < 134217728.0;
+  for (int q = 0; q < 32 && tagOK; ++q)
+    for (int c = 0; c < 32 && tagOK; ++c)
+      if (present[q] && present[c]) {
+        const int64_t v = 4 * ((int64_t)sc->table[q * 32 + c] - (int64_t)a);
+        if (v - 2 < -128 || v - 1 > 127) tagOK = false;
+      }
+  h->tag = tagOK ? 1 : 0;
 
-  // ---- geometry: rows per lane, waves per workgroup
-  int R = h->tuneR ? h->tuneR : (maxn1 <= 256 ? 4 : 8);
-  int W = h->tuneW;
-  if (!W) {
-    const size_t maxStrips = maxn1 ? (maxn1 + 64 * R - 1) / (64 * R) : 1;
-    if (ncomp >= (size_t)4 * h->cus) W = 1;
-    else {
-      const size_t want = ((size_t)16 * h->cus + std::max<size_t>(ncomp, 1) - 1) / std::max<size_t>(ncomp, 1);
-      W = (int)std::min<size_t>({16, maxStrips, want});
-      W = std::max(W, 1);
+  // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair).
+  // Cost model (DESIGN.md "Geometry"): a pair with S strips on W waves runs
+  //   phases = ((S-1)/W) * max(NC, 2W) + 2*((S-1) % W) + NC      chunks of 64 steps,
+  // each step costing ~(8R + 12) VALU issue slots per wave; a CU needs >= 2 waves per SIMD to
+  // fill its issue slots.  Pick the (R, W) with the least estimated time for the batch.
+  int R = 8, W = 1;
+  {
+    const int cand[] = {4, 5, 8, 10};
+    double best = 1e300;
+    for (int Rc : cand) {
+      if (h->tuneR && Rc != h->tuneR) continue;
+      if (!bg_dp_has_R(Rc, h->affine, h->local, h->dna)) continue;
+      const size_t S = maxn1 ? (maxn1 + 64 * Rc - 1) / (64 * Rc) : 1;
+      const int wmax = (h->affine || h->local) ? 8 : 16;
+      for (int Wc = 1; Wc <= wmax; ++Wc) {
+        if (h->tuneW && Wc != h->tuneW) continue;
+        if ((size_t)Wc > S && !h->tuneW) continue;
+        const double NC = (double)(maxn2 / 64 + 2);
+        const double stride = std::max(NC, 2.0 * Wc);
+        const double phases = (double)((S - 1) / Wc) * stride + 2.0 * ((S - 1) % Wc) + NC;
+        // co-resident workgroups per CU (32 waves/CU), sequential rounds of workgroups
+        const double want = std::ceil((double)std::max<size_t>(ncomp, 1) / h->cus);
+        const double wgPerCu = std::max(1.0, std::min(want, std::floor(32.0 / Wc)));
+        const double rounds = std::ceil((double)std::max<size_t>(ncomp, 1) / (h->cus * wgPerCu));
+        // cycles between two instructions of one wave: a wave alone issues every 4 cycles, a
+        // SIMD every 2 cycles shared by its waves
+        const double period = std::max(4.0, 2.0 * Wc * wgPerCu / 4.0);
+        const double t = rounds * phases * 64.0 * (8.0 * Rc + 12.0) * period;
+        if (t < best) { best = t; R = Rc; W = Wc; }
+      }
     }
   }
-  if ((h->affine || h->local) && W > 8) W = 8;  // those kernels are built for <= 512 threads
-  size_t lds = 256;
+  size_t lds = 256;          // lut (+ int16 table and per-wave profiles on the LDS path)
   if (!h->dna) {
     const int WPE = (R + 1) / 2;
     for (;;) {
       lds = 256 + 2048 + (size_t)W * h->kdim * 64 * WPE * 4;
-      if (lds <= 160 * 1024 || W == 1) break;
+      if (lds + 64 <= 160 * 1024 || W == 1) break;
       --W;
     }
+  }
+  h->progOff = (int)lds;     // 16 per-wave progress counters follow
+  lds += 64;
+  // seq2 codes staged in LDS when they fit next to the rest (160 KiB per CU)
+  h->codesOff = (int)lds;
+  {
+    const size_t need = round_up(maxn2 + 16, 16);
+    h->codesInLds = (lds + need <= 160 * 1024) ? 1 : 0;
+    if (h->codesInLds) lds += need;
   }
   h->R = R;
   h->W = W;
@@ -367,7 +418,8 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   h->resBytes = o1 + o2;
 
   // ---- device memory
-  if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->lut.ensure(256) ||
+  if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->codes1.ensure(o1 + 16) ||
+      !h->codes2.ensure(o2 + 16) || !h->lut.ensure(256) ||
       !h->prof.ensure(2048) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)))
     return BG_E_NOMEM;
   for (int z = 0; z < h->depth; ++z) {
@@ -403,6 +455,17 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
         packed |= (uint32_t)(uint8_t)(int8_t)v << (8 * dense[c]);
       }
       prof[dense[q]] = (int32_t)packed;
+      if (h->tag) {
+        uint32_t px = 0, py = 0;
+        for (int c = 0; c < 32; ++c) {
+          if (dense[c] < 0) continue;
+          const int v = 4 * (sc->table[q * 32 + c] - a);
+          px |= (uint32_t)(uint8_t)(int8_t)(v - 1) << (8 * dense[c]);
+          py |= (uint32_t)(uint8_t)(int8_t)(v - 2) << (8 * dense[c]);
+        }
+        prof[64 + dense[q]] = (int32_t)px;
+        prof[128 + dense[q]] = (int32_t)py;
+      }
     }
   } else {
     int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
@@ -410,8 +473,13 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
       for (int c = 0; c < 32; ++c)
         if (dense[q] >= 0 && dense[c] >= 0) t16[dense[q] * 32 + dense[c]] = (int16_t)(sc->table[q * 32 + c] - a);
   }
+  std::vector<uint8_t> cd1(o1 + 1), cd2(o2 + 1);
+  for (uint64_t x = 0; x < o1; ++x) cd1[x] = lut[st1[x]];
+  for (uint64_t x = 0; x < o2; ++x) cd2[x] = lut[st2[x]];
   BG_HIP(hipMemcpyAsync(h->seq1.p, st1.data(), o1 + 1, hipMemcpyHostToDevice, h->stream));
   BG_HIP(hipMemcpyAsync(h->seq2.p, st2.data(), o2 + 1, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->codes1.p, cd1.data(), o1 + 1, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->codes2.p, cd2.data(), o2 + 1, hipMemcpyHostToDevice, h->stream));
   BG_HIP(hipMemcpyAsync(h->lut.p, lut, 256, hipMemcpyHostToDevice, h->stream));
   BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), 2048, hipMemcpyHostToDevice, h->stream));
   if (!h->plan.empty())
@@ -451,13 +519,18 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[0], h->stream));
   if (np) {
-    void* fn = bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
+    void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R) : bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
     A.pairs = h->pairs.as<BgPair>();
     A.seq1 = h->seq1.as<uint8_t>();
     A.seq2 = h->seq2.as<uint8_t>();
     A.lut = h->lut.as<uint8_t>();
+    A.codes1 = h->codes1.as<uint8_t>();
+    A.codes2 = h->codes2.as<uint8_t>();
+    A.prog_off = h->progOff;
+    A.codes_off = h->codesOff;
+    A.codes_in_lds = h->codesInLds;
     A.trace = S.trace.as<uint32_t>();
     A.bndM = S.bndM.as<int32_t>();
     A.bndX = S.bndX.as<int32_t>();
@@ -493,6 +566,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.mode = h->mode;
     F.R = h->R;
     F.affine = h->affine;
+    F.tag = h->tag;
     F.npairs = (int32_t)np;
     void* args[] = {&F};
     BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(h->R, h->affine, h->mode), dim3(np), dim3(256), args,
@@ -606,6 +680,7 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->R = h->R;
   o->waves = h->W;
   o->affine = h->affine;
+  o->tagged = h->tag;
   o->dna = h->dna;
   o->local = h->local;
   o->npairs = (int32_t)h->npairs;

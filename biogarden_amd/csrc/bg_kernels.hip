@@ -113,7 +113,12 @@ struct Ctx {
   int lane;
 };
 
-template <int R, bool AFFINE, bool LOCAL, bool DNA, bool SLOW>
+// Chunk code variants: FAST (interior chunks of every strip but the last), SEL (interior chunks
+// of the last strip when row n1 is not a lane's last row), EDGE (first chunk: column-0 borders;
+// last chunks: column n2 capture / validity; everything general).
+enum { VAR_FAST = 0, VAR_SEL = 1, VAR_EDGE = 2 };
+
+template <int R, bool AFFINE, bool LOCAL, bool DNA, int VAR, bool TAG = false>
 __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx& C, int c, int bM,
                                           int bX, int cv) {
   const int a = C.a;
@@ -127,6 +132,68 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
   for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
     const int u = h * BG_TRACE_BLK + uu;
     const int t = t0 + u;
+    if constexpr (TAG) {
+      // ---- tagged linear-gap step (a >= b, DNA, not local): values are 4*(M + a) with the
+      // tie-break tag in bits 0-1 — D-form tag 0, X-form (from the row above) tag 1, Y-form
+      // (from the left) tag 2 — so v_max3 yields M and the m_trace code (0 'R', 1 'X', 2 'Y'
+      // with priority Y > X > R, aligner.rs:455-463) at once; no SGPR traffic at all.
+      const int topX = dpp_shr1(rdlane(bM, u), S.Xlast);     // X-form of (row above, j)
+      S.code = dpp_shr1(rdlane(cv, u), S.code);
+      int dIn = S.topPrev;                                    // X-form of (row above, j-1)
+      int xo = topX;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int yo = (S.Ma[k] & ~3) | 2;                    // Y-form of (i, j-1)
+        const int d = dIn + sbfe(S.prof[k], S.code, 8);     // 4*(M(i-1,j-1)+S) (tag 0)
+        const int best = imax(imax(d, xo), yo);
+        // append the 2-bit code; the empty asm pins the update here (otherwise LLVM sinks all
+        // 16 alignbits to the flush and keeps every step's `best` live)
+        if (uu < 16) { S.tA[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tA[k], 2); asm volatile("" : "+v"(S.tA[k])); }
+        else { S.tB[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tB[k], 2); asm volatile("" : "+v"(S.tB[k])); }
+        const int T = best + 4 * a;                           // 4*(M(i,j)+a) + tag
+        dIn = yo;
+        xo = (T & ~3) | 1;                                    // X-form for row i+1
+        S.Ma[k] = T;
+      }
+      S.topPrev = topX;
+      S.Xlast = xo;
+      if constexpr (VAR == VAR_EDGE) {
+        if (c == 0) {
+          const bool rst = (t == lane);
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const int i = C.rowbase + k + 1;
+            S.Ma[k] = rst ? 4 * wadd(col0_M(C.mode, i, a, b), a) : S.Ma[k];
+          }
+          S.Xlast = rst ? (S.Ma[R - 1] & ~3) | 1 : S.Xlast;
+        }
+        if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {
+          if (lane == t - C.n2) {
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+              const int i = C.rowbase + k + 1;
+              if (i <= C.n1) C.lastcol[i] = (S.Ma[k] >> 2) - a;
+            }
+          }
+        }
+      }
+      {
+        int sel = S.Xlast;
+        if constexpr (VAR != VAR_FAST) {
+#pragma unroll
+          for (int k = 0; k < R - 1; ++k) sel = (C.orow == k) ? ((S.Ma[k] & ~3) | 1) : sel;
+        }
+        const int jo = t - C.olane;
+        if (VAR != VAR_EDGE || (jo >= 0 && jo <= C.n2)) {
+          S.oM = wrlane(rdlane(sel, C.olane), jo & 63, S.oM);
+          if ((jo & 63) == 63 || (VAR == VAR_EDGE && jo == C.n2)) C.bndOutM[(jo & ~63) + lane] = S.oM;
+        }
+      }
+      // keep each step's independent work (code shift, profile lookups) inside the step: without
+      // this the scheduler hoists all 32 unrolled steps' lookups and spills
+      __builtin_amdgcn_sched_barrier(0);
+      continue;
+    }
     // ---- inputs from the row above: lane r-1's last row at this column, or the boundary row
     const int topMa = dpp_shr1(rdlane(bM, u), S.Ma[R - 1]);
     int topX = 0;
@@ -146,7 +213,7 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
       }
     }
     bool valid = true;
-    if constexpr (SLOW && LOCAL) valid = (t - lane >= 1) && (t - lane <= C.n2);
+    if constexpr (VAR == VAR_EDGE && LOCAL) valid = (t - lane >= 1) && (t - lane <= C.n2);
     int diag = S.topPrev;
     int xo = topMa;
     int xt = topX;
@@ -198,7 +265,7 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
     S.topPrev = topMa;
     if constexpr (AFFINE) S.Xlast = xt;
 
-    if constexpr (SLOW) {
+    if constexpr (VAR == VAR_EDGE) {
       // column 0: this lane is at j == 0 -> load the border (aligner.rs:98-104 / fill(0))
       if (c == 0) {
         const bool rst = (t == lane);
@@ -225,15 +292,15 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
     // ---- boundary output: row `orow` of lane `olane` at column t - olane
     {
       int sel = S.Ma[R - 1];
-      if constexpr (SLOW) {
+      if constexpr (VAR != VAR_FAST) {
 #pragma unroll
         for (int k = 0; k < R - 1; ++k) sel = (C.orow == k) ? S.Ma[k] : sel;
       }
       const int jo = t - C.olane;
-      if (!SLOW || (jo >= 0 && jo <= C.n2)) {
+      if (VAR != VAR_EDGE || (jo >= 0 && jo <= C.n2)) {
         S.oM = wrlane(rdlane(sel, C.olane), jo & 63, S.oM);
         if constexpr (AFFINE) S.oX = wrlane(rdlane(S.Xlast, C.olane), jo & 63, S.oX);
-        if ((jo & 63) == 63 || (SLOW && jo == C.n2)) {
+        if ((jo & 63) == 63 || (VAR == VAR_EDGE && jo == C.n2)) {
           const int blk = jo & ~63;
           C.bndOutM[blk + lane] = S.oM;
           if constexpr (AFFINE) C.bndOutX[blk + lane] = S.oX;
@@ -260,7 +327,7 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
 
 }  // namespace
 
-template <int R, bool AFFINE, bool LOCAL, bool DNA>
+template <int R, bool AFFINE, bool LOCAL, bool DNA, bool TAG = false>
 __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(BgDpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* sLut = smem;                                        // 256 B
@@ -272,17 +339,24 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
   constexpr int ROWS = BG_WAVE * R;
 
   for (int x = threadIdx.x; x < 256; x += blockDim.x) sLut[x] = A.lut[x];
+  if (threadIdx.x < 16) reinterpret_cast<int*>(smem + A.prog_off)[threadIdx.x] = 0;
+  // this pair's seq2 codes, staged once in LDS (every strip sweeps all of them)
+  uint8_t* sCodes = smem + A.codes_off;
+  {
+    const BgPair& Pp = A.pairs[blockIdx.x];
+    const uint8_t* g = A.codes2 + Pp.off2;
+    if (A.codes_in_lds)
+      for (int x = threadIdx.x; x < Pp.n2; x += blockDim.x) sCodes[x] = g[x];
+  }
   if constexpr (!DNA) {
     const int16_t* g = reinterpret_cast<const int16_t*>(A.profile);
     for (int x = threadIdx.x; x < 1024; x += blockDim.x) sTab[x] = g[x];
   }
   __syncthreads();
 
-  const BgPair& P = A.pairs[blockIdx.x];
+  const BgPair P = A.pairs[blockIdx.x];                        // by value: scalar loads, once
   const int n1 = P.n1, n2 = P.n2, nst = P.nstrips, NC = P.nc;
   if (nst == 0) return;
-  const uint8_t* s1 = A.seq1 + P.off1;
-  const uint8_t* s2 = A.seq2 + P.off2;
   const int a = A.open;
   const int b = A.ext;
   const int mode = A.mode;
@@ -299,100 +373,108 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
   C.ldsProf = ldsProf;
 
   Strip<R, AFFINE, LOCAL> S;
-  const int stride = NC > 2 * W ? NC : 2 * W;
-  const int lastS = nst - 1;
-  const int total = (lastS / W) * stride + 2 * (lastS % W) + NC;
-  int s = w;
-  int sstart = 2 * w;
-  int cvNext = 0;
-
-  for (int p = 0; p < total; ++p) {
-    if (s < nst && p >= sstart) {
-      const int c = p - sstart;
-      if (c == 0) {
-        // ---------------- strip begin
-        C.s = s;
-        C.rowbase = s * ROWS + lane * R;
-        const bool lastStrip = (s == nst - 1);
-        const int lastRow = n1 - 1 - s * ROWS;                 // row n1, 0-based within the strip
-        C.olane = lastStrip ? lastRow / R : BG_WAVE - 1;
-        C.orow = lastStrip ? lastRow % R : R - 1;
-        C.trace = A.trace + P.trace_off / 4 + (size_t)s * stripDw;
-        C.bndOutM = A.bndM + P.bnd_off + (size_t)s * NC * BG_CHUNK;
-        C.bndOutX = AFFINE ? A.bndX + P.bnd_off + (size_t)s * NC * BG_CHUNK : nullptr;
+  const uint8_t* c1 = A.codes1 + P.off1;
+  const uint8_t* c2 = A.codes2 + P.off2;
+  const int nblk = NC - 1;                                     // boundary blocks per strip
+  // Strips are pipelined through per-wave progress counters in LDS (no workgroup barriers):
+  // after chunk c of its rho-th strip a wave publishes rho*nblk + (blocks of this strip stored);
+  // strip s waits before chunk c until strip s-1 has stored boundary block c.
+  int* sProg = reinterpret_cast<int*>(smem + A.prog_off);
+  for (int s = w, rho = 0; s < nst; s += W, ++rho) {
+    // ---------------- strip begin
+    C.s = s;
+    C.rowbase = s * ROWS + lane * R;
+    const bool lastStrip = (s == nst - 1);
+    const int lastRow = n1 - 1 - s * ROWS;                 // row n1, 0-based within the strip
+    C.olane = lastStrip ? lastRow / R : BG_WAVE - 1;
+    C.orow = lastStrip ? lastRow % R : R - 1;
+    const bool selRow = C.orow != R - 1;
+    C.trace = A.trace + P.trace_off / 4 + (size_t)s * stripDw;
+    C.bndOutM = A.bndM + P.bnd_off + (size_t)s * NC * BG_CHUNK;
+    C.bndOutX = AFFINE ? A.bndX + P.bnd_off + (size_t)s * NC * BG_CHUNK : nullptr;
+    int qk[R];
 #pragma unroll
-        for (int k = 0; k < R; ++k) {
-          const int i = C.rowbase + k + 1;                       // 1-based row
-          const int q = (i <= n1) ? sLut[s1[i - 1]] : 0;
-          if constexpr (DNA) S.prof[k] = A.profile[q >> 3];
-          S.Ma[k] = wadd(col0_M(mode, i, a, b), a);
-          if constexpr (AFFINE) { S.Y[k] = kNegInf; S.tC[k] = 0; S.tD[k] = 0; }
-          S.tA[k] = 0; S.tB[k] = 0;
-          if constexpr (LOCAL) { S.bestv[k] = (i <= n1) ? INT32_MIN : INT32_MAX; S.bpos[k] = 0; }
-        }
-        if constexpr (!DNA) {
-          // per-lane table [code][lane] of R int16 S(q_k, code) - a, 2R bytes per entry
-          constexpr int WPE = (R + 1) / 2;
-          for (int cd = 0; cd < A.kdim; ++cd) {
+    for (int k = 0; k < R; ++k) {                              // independent loads, no branches
+      const int i = C.rowbase + k + 1;
+      qk[k] = c1[(i <= n1 ? i : n1) - 1];
+    }
 #pragma unroll
-            for (int q2 = 0; q2 < WPE; ++q2) {
-              int v = 0;
+    for (int k = 0; k < R; ++k) {
+      const int i = C.rowbase + k + 1;                       // 1-based row
+      const int q = (i <= n1) ? qk[k] : 0;
+      if constexpr (TAG) S.prof[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];  // 4(S-a)-1 / 4(S-a)-2
+      else if constexpr (DNA) S.prof[k] = A.profile[q >> 3];
+      S.Ma[k] = TAG ? 4 * wadd(col0_M(mode, i, a, b), a) : wadd(col0_M(mode, i, a, b), a);
+      if constexpr (AFFINE) { S.Y[k] = kNegInf; S.tC[k] = 0; S.tD[k] = 0; }
+      S.tA[k] = 0; S.tB[k] = 0;
+      if constexpr (LOCAL) { S.bestv[k] = (i <= n1) ? INT32_MIN : INT32_MAX; S.bpos[k] = 0; }
+    }
+    if constexpr (!DNA) {
+      // per-lane table [code][lane] of R int16 S(q_k, code) - a, 2R bytes per entry
+      constexpr int WPE = (R + 1) / 2;
+      for (int cd = 0; cd < A.kdim; ++cd) {
 #pragma unroll
-              for (int h = 0; h < 2; ++h) {
-                const int k = q2 * 2 + h;
-                if (k < R) {
-                  const int i = C.rowbase + k + 1;
-                  const int qq = (i <= n1) ? sLut[s1[i - 1]] : 0;
-                  v |= ((int)(uint16_t)sTab[qq * 32 + cd]) << (16 * h);
-                }
-              }
-              ldsProf[(cd * BG_WAVE + lane) * WPE + q2] = v;
+        for (int q2 = 0; q2 < WPE; ++q2) {
+          int v = 0;
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const int k = q2 * 2 + hh;
+            if (k < R) {
+              const int i = C.rowbase + k + 1;
+              const int qq = (i <= n1) ? c1[i - 1] : 0;
+              v |= ((int)(uint16_t)sTab[qq * 32 + cd]) << (16 * hh);
             }
           }
-        }
-        S.topPrev = 0; S.Xlast = kNegInf; S.code = 0; S.oM = 0; S.oX = 0;
-        {
-          const int j = lane;                                   // codes of chunk 0
-          cvNext = (j >= 1 && j <= n2) ? sLut[s2[j - 1]] : 0;
+          ldsProf[(cd * BG_WAVE + lane) * WPE + q2] = v;
         }
       }
-      // ---------------- chunk c: inputs
-      const int cv = cvNext;
+    }
+    S.topPrev = 0; S.Xlast = TAG ? 1 : kNegInf; S.code = 0; S.oM = 0; S.oX = 0;
+    // residue codes of seq2, two chunks in flight: column j = c*64 + lane uses seq2[j-1]
+    for (int c = 0; c < NC; ++c) {
+      int cv;
       {
-        const int j = (c + 1) * BG_CHUNK + lane;                 // prefetch codes of chunk c+1
-        cvNext = (j >= 1 && j <= n2) ? sLut[s2[j - 1]] : 0;
+        const int j = c * BG_CHUNK + lane;
+        const int jj = j < 1 ? 1 : (j > n2 ? n2 : j);
+        const int v = A.codes_in_lds ? (int)sCodes[jj - 1] : (int)c2[jj - 1];
+        cv = (j >= 1 && j <= n2) ? v : 0;
       }
       const int jb = c * BG_CHUNK + lane;
       int bM, bX = kNegInf;
       if (s == 0) {
         bM = wadd(row0_M(mode, jb, a, b), a);
+        if constexpr (TAG) bM = 4 * bM + 1;                    // X-form of row 0
       } else {
+        if (c < nblk) {                                        // block c of strip s-1
+          const int need = ((s - 1) / W) * nblk + c + 1;
+          const int pw = (s - 1) % W;
+          while (__hip_atomic_load(sProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+            __builtin_amdgcn_s_sleep(1);
+        }
         const int32_t* src = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb;
         bM = load_agent(src);
         if constexpr (AFFINE) bX = load_agent(A.bndX + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
       }
-      const bool slow = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2) || (s == nst - 1);
-      if (slow) run_chunk<R, AFFINE, LOCAL, DNA, true>(S, C, c, bM, bX, cv);
-      else run_chunk<R, AFFINE, LOCAL, DNA, false>(S, C, c, bM, bX, cv);
-
-      if (c == NC - 1) {
-        // ---------------- strip end
-        if constexpr (LOCAL) {
-          int32_t* rowbest = A.aux + P.aux_off + (n1 + 1);
-          int32_t* rowpos = rowbest + n1;
-#pragma unroll
-          for (int k = 0; k < R; ++k) {
-            const int i = C.rowbase + k + 1;
-            if (i <= n1) { rowbest[i - 1] = S.bestv[k]; rowpos[i - 1] = S.bpos[k] - lane; }
-          }
-        }
-        s += W;
-        sstart += stride;
-      }
+      const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
+      if (edge) run_chunk<R, AFFINE, LOCAL, DNA, VAR_EDGE, TAG>(S, C, c, bM, bX, cv);
+      else if (lastStrip && selRow) run_chunk<R, AFFINE, LOCAL, DNA, VAR_SEL, TAG>(S, C, c, bM, bX, cv);
+      else run_chunk<R, AFFINE, LOCAL, DNA, VAR_FAST, TAG>(S, C, c, bM, bX, cv);
+      // publish: the chunk ends with the R trace stores of its second half; everything issued
+      // before them (this chunk's boundary-row stores included) has reached L2 at vmcnt(R)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
+      if (lane == 0)
+        __hip_atomic_store(sProg + w, rho * nblk + (c < nblk ? c : nblk), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (W > 1) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // boundary stores visible before the barrier
-      __syncthreads();
+    // ---------------- strip end
+    if constexpr (LOCAL) {
+      int32_t* rowbest = A.aux + P.aux_off + (n1 + 1);
+      int32_t* rowpos = rowbest + n1;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int i = C.rowbase + k + 1;
+        if (i <= n1) { rowbest[i - 1] = S.bestv[k]; rowpos[i - 1] = S.bpos[k] - lane; }
+      }
     }
   }
 }
@@ -414,7 +496,8 @@ struct Fin {
 __device__ __forceinline__ int lastrowM(const Fin& f, int j) {
   if (f.n1 == 0) return row0_M(f.mode, j, f.a, f.b);
   if (j == 0) return col0_M(f.mode, f.n1, f.a, f.b);
-  return wadd(f.lastrowMa[j], -f.a);
+  const int v = f.lastrowMa[j];
+  return f.F->tag ? (v >> 2) - f.a : wadd(v, -f.a);    // tagged kernel stores 4(M+a)+1
 }
 __device__ __forceinline__ int lastcolM(const Fin& f, int i) {
   if (f.n2 == 0) return col0_M(f.mode, i, f.a, f.b);
@@ -447,8 +530,7 @@ template <int R, bool AFFINE, int MODE>
 __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int NW = AFFINE ? 4 : 2;
-  constexpr int LOGR = (R == 4) ? 2 : 3;
-  constexpr int LOGROWS = 6 + LOGR;
+  constexpr int ROWS = BG_WAVE * R;
   constexpr int BLK_DW = R * BG_WAVE * NW;             // dwords per 32-step trace block
   constexpr int NBW = kWinBytes / (BLK_DW * 4);        // blocks per window
   uint32_t* win = reinterpret_cast<uint32_t*>(smem);
@@ -580,7 +662,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             codes = kCodeBorder | ((kk == 0) ? 2 : 1);  // m_trace borders: column 0 'X', row 0 'Y'
           } else {
             const int vr = kk - 1;
-            const int sidx = vr >> LOGROWS, r = (vr >> LOGR) & 63, q = vr & (R - 1);
+            const int sidx = vr / ROWS, rem = vr - sidx * ROWS, r = rem / R, q = rem - r * R;
             const int t = ll + r, bl = t >> 5;
             if (sidx != curS || bl < curB0 || bl >= curB0 + curNb) {
               codes = kCodeMiss;
@@ -591,6 +673,10 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
               if constexpr (AFFINE) {
                 const uint4 v = *reinterpret_cast<const uint4*>(wp);
                 c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | (((v.z >> bit) & 1) << 2) | (((v.w >> bit) & 1) << 3);
+              } else if (F.tag) {
+                const uint2 v = *reinterpret_cast<const uint2*>(wp);  // 2-bit codes, 16 steps/word
+                const int u = t & 31;
+                c = (int)(((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3) | 12;
               } else {
                 const uint2 v = *reinterpret_cast<const uint2*>(wp);
                 c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | 12;
@@ -602,8 +688,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         const int c = rdlane(codes, dk * 8 + dl);
         if (c & kCodeMiss) {
           const int vr = k - 1;
-          reqS = vr >> LOGROWS;
-          const int bl = (l + ((vr >> LOGR) & 63)) >> 5;
+          reqS = vr / ROWS;
+          const int bl = (l + (vr - reqS * ROWS) / R) >> 5;
           reqB0 = bl - NBW + 1 > 0 ? bl - NBW + 1 : 0;
           break;
         }
@@ -765,6 +851,26 @@ typedef void (*bg_dp_fn)(BgDpArgs);
 
 BG_INST_R(4)
 BG_INST_R(8)
+// metric-path (linear gaps, DNA register profile) kernels at extra strip heights: the planner
+// picks R so that a pair's strip count fills the workgroup's waves (DESIGN.md "Geometry")
+BG_INST(5, false, false, true)
+BG_INST(10, false, false, true)
+template __global__ void bg_dp_kernel<4, false, false, true, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<5, false, false, true, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<8, false, false, true, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<10, false, false, true, true>(BgDpArgs);
+BG_INST(5, false, true, true)
+BG_INST(10, false, true, true)
+
+extern "C" void* bg_dp_kernel_tag_ptr(int R) {
+  switch (R) {
+    case 4: return (void*)&bg_dp_kernel<4, false, false, true, true>;
+    case 5: return (void*)&bg_dp_kernel<5, false, false, true, true>;
+    case 8: return (void*)&bg_dp_kernel<8, false, false, true, true>;
+    case 10: return (void*)&bg_dp_kernel<10, false, false, true, true>;
+    default: return nullptr;
+  }
+}
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna) {
 #define BG_PICK(RR)                                                                        \
@@ -781,6 +887,10 @@ extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna) {
   BG_PICK(4)
   BG_PICK(8)
 #undef BG_PICK
+  if (!affine && dna && (R == 5 || R == 10)) {
+    if (R == 5) return local ? (void*)&bg_dp_kernel<5, false, true, true> : (void*)&bg_dp_kernel<5, false, false, true>;
+    return local ? (void*)&bg_dp_kernel<10, false, true, true> : (void*)&bg_dp_kernel<10, false, false, true>;
+  }
   return nullptr;
 }
 
@@ -797,6 +907,13 @@ static void* finish_ptr(int mode) {
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode) {
   if (R == 4) return affine ? finish_ptr<4, true>(mode) : finish_ptr<4, false>(mode);
   if (R == 8) return affine ? finish_ptr<8, true>(mode) : finish_ptr<8, false>(mode);
+  if (R == 5 && !affine) return finish_ptr<5, false>(mode);
+  if (R == 10 && !affine) return finish_ptr<10, false>(mode);
   return nullptr;
+}
+
+// Which strip heights exist for a kernel family (the planner's candidate set).
+extern "C" int bg_dp_has_R(int R, int affine, int local, int dna) {
+  return bg_dp_kernel_ptr(R, affine, local, dna) != nullptr;
 }
 extern "C" size_t bg_finish_lds_bytes() { return kWinBytes + 64 * 4 + 2 * 256 * 4; }

@@ -126,6 +126,7 @@ typedef struct bg_stats {
   int32_t R;               /* rows per lane */
   int32_t waves;           /* waves per workgroup (one workgroup per pair) */
   int32_t affine;          /* 1: affine kernel (open < extend), 0: linear-gap kernel */
+  int32_t tagged;          /* 1: tagged linear kernel (tie-break tag in the score's low bits) */
   int32_t dna;             /* 1: register profile (<= 4 symbols), 0: LDS profile */
   int32_t local;
   int32_t npairs;
@@ -154,6 +155,10 @@ int bg_set_tuning(bg_aligner* h, int R, int waves);
  * kernel of execute k overlaps the DP kernel of execute k+1 (two HIP streams); 1 serialises.
  * Takes effect at the next bg_batch_prepare. */
 int bg_set_pipeline(bg_aligner* h, int depth);
+
+/* allow_tagged = 0 forces the mask-trace kernel where the tagged linear kernel would be used
+ * (tests compare both).  Takes effect at the next bg_batch_prepare. */
+int bg_set_kernel_options(bg_aligner* h, int allow_tagged);
 
 const char* bg_status_string(int status);
 int bg_abi_version(void);

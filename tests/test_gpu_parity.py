@@ -168,6 +168,27 @@ def test_geometries_multistrip(aligner, oracle, R, W, mode, a, b):
         aligner.set_tuning(0, 0)
 
 
+@pytest.mark.parametrize("tagged", [True, False])
+@pytest.mark.parametrize("R,W", [(4, 3), (5, 1), (5, 8), (8, 16), (10, 2), (10, 16)])
+@pytest.mark.parametrize("mode", ["semiglobal", "local", "overlap", "fitting", "global"])
+def test_geometries_linear_dna(aligner, oracle, R, W, mode, tagged):
+    """The metric-path kernels (linear gaps a >= b, DNA register profile) at every strip height,
+    tagged (tie-break tag in the score) and mask-trace variants."""
+    rng = random.Random(R * 1000 + W)
+    aligner._h.set_kernel_options(tagged)
+    aligner.set_tuning(R, W)
+    try:
+        pairs = []
+        for n1, n2 in ((1500, 1400), (700, 2100), (64 * R * 3 + 1, 333), (640, 640), (2, 5), (2100, 2100)):
+            s1 = rand_seq(rng, n1, DNA)
+            s2 = mutate(rng, s1, DNA, 0.15)[:n2]
+            pairs.append((s1, s2))
+        check_batch(aligner, oracle, mode, pairs, "blosum62", -1, -2, fresh=False)
+    finally:
+        aligner.set_tuning(0, 0)
+        aligner._h.set_kernel_options(True)
+
+
 def test_buffer_edge_and_divergence(aligner, oracle):
     """Lengths around the reference's 1024x1024 default scratch (A.7)."""
     rng = random.Random(7)
