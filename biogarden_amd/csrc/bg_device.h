@@ -78,6 +78,7 @@ struct BgDpArgs {
   int32_t prog_off;        // byte offset of the 16 per-wave progress counters in dynamic LDS
   int32_t codes_off;       // byte offset of the staged seq2 codes in dynamic LDS
   int32_t codes_in_lds;    // 1 if every pair's seq2 fits there
+  int32_t aux_lds_off;     // tagged kernel: per-wave boundary block + output ring (1280 B/wave)
 };
 
 struct BgFinishArgs {

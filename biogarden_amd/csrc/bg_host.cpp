@@ -97,6 +97,7 @@ struct bg_aligner {
   int progOff = 256;
   int codesOff = 320;
   int codesInLds = 0;
+  int auxLdsOff = 0;
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
   float dp_ms = 0.f, fin_ms = 0.f;
@@ -368,9 +369,17 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   // seq2 codes staged in LDS when they fit next to the rest (160 KiB per CU)
   h->codesOff = (int)lds;
   {
-    const size_t need = round_up(maxn2 + 16, 16);
+    // the tagged kernel reads codes at (t - lane - 1) unclamped: 64 bytes of slack before the
+    // row (the counters/lut) and up to 127 after it
+    const size_t need = round_up(maxn2 + (h->tag ? 256 : 16), 16);
     h->codesInLds = (lds + need <= 160 * 1024) ? 1 : 0;
     if (h->codesInLds) lds += need;
+  }
+  h->auxLdsOff = (int)lds;
+  if (h->tag) {
+    const size_t ring = (size_t)W * (64 + 256) * 4;   // boundary block + output ring per wave
+    if (!h->codesInLds || lds + ring > 160 * 1024) h->tag = 0;
+    else lds += ring;
   }
   h->R = R;
   h->W = W;
@@ -531,6 +540,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.prog_off = h->progOff;
     A.codes_off = h->codesOff;
     A.codes_in_lds = h->codesInLds;
+    A.aux_lds_off = h->auxLdsOff;
     A.trace = S.trace.as<uint32_t>();
     A.bndM = S.bndM.as<int32_t>();
     A.bndX = S.bndX.as<int32_t>();

@@ -23,65 +23,11 @@
 
 #include "bg_device.h"
 
-typedef unsigned long long u64;
+#include "bg_dev_util.h"
 
-extern "C" __device__ int bg_writelane_i32(int src, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+using namespace bgk;
 
 namespace {
-
-constexpr int kNegInf = INT32_MIN;  // i32::MIN: x/y buffers' initial value (aligner.rs:49-50)
-
-__device__ __forceinline__ int dpp_shr1(int old, int src) {
-  // v_mov_b32_dpp wave_shr:1 — lane r receives lane r-1; lane 0 keeps `old`.
-  return __builtin_amdgcn_update_dpp(old, src, 0x138, 0xf, 0xf, false);
-}
-__device__ __forceinline__ int rdlane(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ int wrlane(int val, int l, int old) { return bg_writelane_i32(val, l, old); }
-__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
-// release-mode i32 `+` wraps; `saturating_add` is v_add_i32 ... clamp
-__device__ __forceinline__ int wadd(int x, int y) { return (int)((unsigned)x + (unsigned)y); }
-__device__ __forceinline__ int wmul(int x, int y) { return (int)((unsigned)x * (unsigned)y); }
-__device__ __forceinline__ int sadd(int x, int y) { return __builtin_elementwise_add_sat(x, y); }
-__device__ __forceinline__ int imax(int x, int y) { return __builtin_elementwise_max(x, y); }
-// v_max3_i32 kept opaque so the compiler cannot turn `best == y` into a max+compare pair.
-__device__ __forceinline__ int imax3(int x, int y, int z) {
-  int r;
-  asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
-  return r;
-}
-__device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
-__device__ __forceinline__ int sbfe(int v, int off, int w) { return __builtin_amdgcn_sbfe(v, off, w); }
-
-// acc = 2*acc + (this lane's bit of mask): one VALU op per trace bit.
-__device__ __forceinline__ unsigned shift_in(unsigned acc, u64 mask) {
-  unsigned r;
-  u64 co;
-  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(acc), "s"(mask));
-  return r;
-}
-
-// v_cndmask_b32 kept opaque: a plain `gt ? best : old` chain over the unrolled steps is
-// re-associated by LLVM into a max-tree that keeps every step's value live (register spills).
-__device__ __forceinline__ int vsel(u64 mask, int if_set, int if_clear) {
-  int r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(mask));
-  return r;
-}
-
-__device__ __forceinline__ int load_agent(const int32_t* p) {
-  // L1-bypassing load (global_load_dword sc1): boundary rows written by another wave.
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Row 0 / column 0 initialisation per mode (aligner.rs:96-104, 163, 233-237, 299, 360).
-__device__ __forceinline__ int row0_M(int mode, int j, int a, int b) {
-  if (j == 0) return 0;
-  return (mode == BGK_GLOBAL || mode == BGK_FITTING) ? wadd(a, wmul(j - 1, b)) : 0;
-}
-__device__ __forceinline__ int col0_M(int mode, int i, int a, int b) {
-  if (i == 0) return 0;
-  return (mode == BGK_GLOBAL) ? wadd(a, wmul(i - 1, b)) : 0;
-}
 
 template <int R, bool AFFINE, bool LOCAL>
 struct Strip {
@@ -118,7 +64,7 @@ struct Ctx {
 // last chunks: column n2 capture / validity; everything general).
 enum { VAR_FAST = 0, VAR_SEL = 1, VAR_EDGE = 2 };
 
-template <int R, bool AFFINE, bool LOCAL, bool DNA, int VAR, bool TAG = false>
+template <int R, bool AFFINE, bool LOCAL, bool DNA, int VAR>
 __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx& C, int c, int bM,
                                           int bX, int cv) {
   const int a = C.a;
@@ -132,68 +78,6 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
   for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
     const int u = h * BG_TRACE_BLK + uu;
     const int t = t0 + u;
-    if constexpr (TAG) {
-      // ---- tagged linear-gap step (a >= b, DNA, not local): values are 4*(M + a) with the
-      // tie-break tag in bits 0-1 — D-form tag 0, X-form (from the row above) tag 1, Y-form
-      // (from the left) tag 2 — so v_max3 yields M and the m_trace code (0 'R', 1 'X', 2 'Y'
-      // with priority Y > X > R, aligner.rs:455-463) at once; no SGPR traffic at all.
-      const int topX = dpp_shr1(rdlane(bM, u), S.Xlast);     // X-form of (row above, j)
-      S.code = dpp_shr1(rdlane(cv, u), S.code);
-      int dIn = S.topPrev;                                    // X-form of (row above, j-1)
-      int xo = topX;
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        const int yo = (S.Ma[k] & ~3) | 2;                    // Y-form of (i, j-1)
-        const int d = dIn + sbfe(S.prof[k], S.code, 8);     // 4*(M(i-1,j-1)+S) (tag 0)
-        const int best = imax(imax(d, xo), yo);
-        // append the 2-bit code; the empty asm pins the update here (otherwise LLVM sinks all
-        // 16 alignbits to the flush and keeps every step's `best` live)
-        if (uu < 16) { S.tA[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tA[k], 2); asm volatile("" : "+v"(S.tA[k])); }
-        else { S.tB[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tB[k], 2); asm volatile("" : "+v"(S.tB[k])); }
-        const int T = best + 4 * a;                           // 4*(M(i,j)+a) + tag
-        dIn = yo;
-        xo = (T & ~3) | 1;                                    // X-form for row i+1
-        S.Ma[k] = T;
-      }
-      S.topPrev = topX;
-      S.Xlast = xo;
-      if constexpr (VAR == VAR_EDGE) {
-        if (c == 0) {
-          const bool rst = (t == lane);
-#pragma unroll
-          for (int k = 0; k < R; ++k) {
-            const int i = C.rowbase + k + 1;
-            S.Ma[k] = rst ? 4 * wadd(col0_M(C.mode, i, a, b), a) : S.Ma[k];
-          }
-          S.Xlast = rst ? (S.Ma[R - 1] & ~3) | 1 : S.Xlast;
-        }
-        if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {
-          if (lane == t - C.n2) {
-#pragma unroll
-            for (int k = 0; k < R; ++k) {
-              const int i = C.rowbase + k + 1;
-              if (i <= C.n1) C.lastcol[i] = (S.Ma[k] >> 2) - a;
-            }
-          }
-        }
-      }
-      {
-        int sel = S.Xlast;
-        if constexpr (VAR != VAR_FAST) {
-#pragma unroll
-          for (int k = 0; k < R - 1; ++k) sel = (C.orow == k) ? ((S.Ma[k] & ~3) | 1) : sel;
-        }
-        const int jo = t - C.olane;
-        if (VAR != VAR_EDGE || (jo >= 0 && jo <= C.n2)) {
-          S.oM = wrlane(rdlane(sel, C.olane), jo & 63, S.oM);
-          if ((jo & 63) == 63 || (VAR == VAR_EDGE && jo == C.n2)) C.bndOutM[(jo & ~63) + lane] = S.oM;
-        }
-      }
-      // keep each step's independent work (code shift, profile lookups) inside the step: without
-      // this the scheduler hoists all 32 unrolled steps' lookups and spills
-      __builtin_amdgcn_sched_barrier(0);
-      continue;
-    }
     // ---- inputs from the row above: lane r-1's last row at this column, or the boundary row
     const int topMa = dpp_shr1(rdlane(bM, u), S.Ma[R - 1]);
     int topX = 0;
@@ -327,7 +211,7 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
 
 }  // namespace
 
-template <int R, bool AFFINE, bool LOCAL, bool DNA, bool TAG = false>
+template <int R, bool AFFINE, bool LOCAL, bool DNA>
 __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(BgDpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* sLut = smem;                                        // 256 B
@@ -402,9 +286,8 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
     for (int k = 0; k < R; ++k) {
       const int i = C.rowbase + k + 1;                       // 1-based row
       const int q = (i <= n1) ? qk[k] : 0;
-      if constexpr (TAG) S.prof[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];  // 4(S-a)-1 / 4(S-a)-2
-      else if constexpr (DNA) S.prof[k] = A.profile[q >> 3];
-      S.Ma[k] = TAG ? 4 * wadd(col0_M(mode, i, a, b), a) : wadd(col0_M(mode, i, a, b), a);
+      if constexpr (DNA) S.prof[k] = A.profile[q >> 3];
+      S.Ma[k] = wadd(col0_M(mode, i, a, b), a);
       if constexpr (AFFINE) { S.Y[k] = kNegInf; S.tC[k] = 0; S.tD[k] = 0; }
       S.tA[k] = 0; S.tB[k] = 0;
       if constexpr (LOCAL) { S.bestv[k] = (i <= n1) ? INT32_MIN : INT32_MAX; S.bpos[k] = 0; }
@@ -429,7 +312,7 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
         }
       }
     }
-    S.topPrev = 0; S.Xlast = TAG ? 1 : kNegInf; S.code = 0; S.oM = 0; S.oX = 0;
+    S.topPrev = 0; S.Xlast = kNegInf; S.code = 0; S.oM = 0; S.oX = 0;
     // residue codes of seq2, two chunks in flight: column j = c*64 + lane uses seq2[j-1]
     for (int c = 0; c < NC; ++c) {
       int cv;
@@ -443,7 +326,6 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
       int bM, bX = kNegInf;
       if (s == 0) {
         bM = wadd(row0_M(mode, jb, a, b), a);
-        if constexpr (TAG) bM = 4 * bM + 1;                    // X-form of row 0
       } else {
         if (c < nblk) {                                        // block c of strip s-1
           const int need = ((s - 1) / W) * nblk + c + 1;
@@ -456,9 +338,9 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
         if constexpr (AFFINE) bX = load_agent(A.bndX + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
       }
       const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
-      if (edge) run_chunk<R, AFFINE, LOCAL, DNA, VAR_EDGE, TAG>(S, C, c, bM, bX, cv);
-      else if (lastStrip && selRow) run_chunk<R, AFFINE, LOCAL, DNA, VAR_SEL, TAG>(S, C, c, bM, bX, cv);
-      else run_chunk<R, AFFINE, LOCAL, DNA, VAR_FAST, TAG>(S, C, c, bM, bX, cv);
+      if (edge) run_chunk<R, AFFINE, LOCAL, DNA, VAR_EDGE>(S, C, c, bM, bX, cv);
+      else if (lastStrip && selRow) run_chunk<R, AFFINE, LOCAL, DNA, VAR_SEL>(S, C, c, bM, bX, cv);
+      else run_chunk<R, AFFINE, LOCAL, DNA, VAR_FAST>(S, C, c, bM, bX, cv);
       // publish: the chunk ends with the R trace stores of its second half; everything issued
       // before them (this chunk's boundary-row stores included) has reached L2 at vmcnt(R)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
@@ -855,22 +737,8 @@ BG_INST_R(8)
 // picks R so that a pair's strip count fills the workgroup's waves (DESIGN.md "Geometry")
 BG_INST(5, false, false, true)
 BG_INST(10, false, false, true)
-template __global__ void bg_dp_kernel<4, false, false, true, true>(BgDpArgs);
-template __global__ void bg_dp_kernel<5, false, false, true, true>(BgDpArgs);
-template __global__ void bg_dp_kernel<8, false, false, true, true>(BgDpArgs);
-template __global__ void bg_dp_kernel<10, false, false, true, true>(BgDpArgs);
 BG_INST(5, false, true, true)
 BG_INST(10, false, true, true)
-
-extern "C" void* bg_dp_kernel_tag_ptr(int R) {
-  switch (R) {
-    case 4: return (void*)&bg_dp_kernel<4, false, false, true, true>;
-    case 5: return (void*)&bg_dp_kernel<5, false, false, true, true>;
-    case 8: return (void*)&bg_dp_kernel<8, false, false, true, true>;
-    case 10: return (void*)&bg_dp_kernel<10, false, false, true, true>;
-    default: return nullptr;
-  }
-}
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna) {
 #define BG_PICK(RR)                                                                        \

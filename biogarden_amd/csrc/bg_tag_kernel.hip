@@ -1,0 +1,254 @@
+// Tagged linear-gap DP kernel: the metric path (semiglobal / global / fitting / overlap,
+// a >= b, DNA-sized alphabets).  Replaces compute_scores_global (src/alignment/aligner.rs:437-469)
+// for the case where the x/y gap matrices provably collapse onto M.
+//
+// Same strip geometry and trace layout as bg_dp_kernel (one workgroup per pair, W waves, strips
+// of 64*R rows, lane r owns rows [rR, rR+R), anti-diagonal sweep with lane r at column t - r),
+// but everything per step that is not cell arithmetic is moved off the VALU:
+//
+//   * values are kept as 4*(M + a) + tag, tag 0 for the diagonal form, 1 for the X form (from
+//     the row above) and 2 for the Y form (from the left), so one v_max3 yields M and the
+//     m_trace code with the reference's tie priority Y > X > R (aligner.rs:455-463);
+//   * the column code is read by every lane from the pair's code row in LDS at (t - lane - 1)
+//     with a compile-time immediate offset per step (ds_read_u8, no VALU);
+//   * the row above of lane 0 (the boundary row of the strip above) is staged per 64-column
+//     block in LDS and read as a broadcast per step, feeding the `old` operand of the one DPP
+//     wave_shr:1 that moves each lane's last row down to the next lane;
+//   * the boundary row this strip hands to the strip below is written by EVERY lane into an LDS
+//     ring at slot (u + 64 - lane): position p = t - lane receives its final value from the
+//     last lane that writes it — lane 63 (or the lane holding row n1 in the last strip; lanes
+//     below it write to a dummy half of the ring) — and each finished 64-column block is
+//     copied to HBM once per chunk.  No v_readlane / v_writelane in the loop.
+//
+// Per cell: v_bfe (profile byte), v_add, v_max3, v_alignbit (2-bit trace code), v_and, 2x v_add.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bg_dev_util.h"
+
+using namespace bgk;
+
+namespace {
+
+template <int R>
+struct TagStrip {
+  int Y[R];           // Y form of (i_k, j-1): 4*(M(i_k, j-1) + a) + 2
+  unsigned tA[R];     // trace codes of steps 0-15 of the current 32-step block (2 bits each)
+  unsigned tB[R];     // steps 16-31
+  int prof[R];        // 4 packed int8: 4(S(q_k, c) - a) - 1 (row 0 of the lane) or - 2
+  int topPrev;        // X form of (row above, j-1) for the lane's first row
+  int Xlast;          // X form of (lane's last row, j): handed down to lane r+1 by DPP
+};
+
+struct TagCtx {
+  int a, b, mode, n1, n2, rowbase, orow, lane;
+  uint32_t* trace;          // this strip's trace
+  int32_t* bndOut;          // this strip's boundary row (X forms), 64-column blocks
+  int32_t* lastcol;         // M(i, n2)
+  const int* bIn;           // LDS: staged boundary block of the strip above (64 X forms)
+  int* ring;                // LDS: this wave's 256-slot output ring
+  int* oLane;               // LDS: this lane's ring write base (slot = u + 64 - lane [+128])
+  const uint8_t* codeLane;  // LDS: code row + t0 - lane - 1 (this chunk)
+};
+
+enum { TV_FAST = 0, TV_SEL = 1, TV_EDGE = 2 };
+
+template <int R, int VAR>
+__device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c) {
+  const int a = C.a;
+  const int a4x = 4 * a + 1;     // bm + a4x = X form, bm + a4x + 1 = Y form
+  const int t0 = c * BG_CHUNK;
+  const int lane = C.lane;
+  int nTop = C.bIn[0];
+  int nCode = C.codeLane[0];
+#pragma unroll 1
+  for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h) {
+#pragma unroll
+    for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
+      const int u = h * BG_TRACE_BLK + uu;
+      const int t = t0 + u;
+      const int topIn = nTop;
+      const int code = nCode;
+      if (uu + 1 < BG_TRACE_BLK) {       // next step's operands are in flight during this one
+        nTop = C.bIn[u + 1];
+        nCode = C.codeLane[u + 1];
+      } else if (h == 0) {
+        nTop = C.bIn[BG_TRACE_BLK];
+        nCode = C.codeLane[BG_TRACE_BLK];
+      }
+      const int topX = dpp_shr1(topIn, S.Xlast);             // X form of (row above, j)
+      int dIn = S.topPrev;                                    // X form of (row above, j-1)
+      int xo = topX;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int yo = S.Y[k];
+        const int d = dIn + sbfe(S.prof[k], code, 8);         // 4*(M(i-1,j-1) + S), tag 0
+        const int best = imax(imax(d, xo), yo);
+        // append the 2-bit code; the empty asm pins each update to its step (otherwise LLVM
+        // sinks all 16 alignbits to the flush and keeps every step's `best` live)
+        if (uu < 16) { S.tA[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tA[k], 2); asm volatile("" : "+v"(S.tA[k])); }
+        else { S.tB[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tB[k], 2); asm volatile("" : "+v"(S.tB[k])); }
+        const int bm = best & ~3;                             // 4*M(i,j) - 4a
+        dIn = yo;
+        xo = bm + a4x;                                        // X form for row i+1
+        S.Y[k] = bm + (a4x + 1);                              // Y form for column j+1
+      }
+      S.topPrev = topX;
+      S.Xlast = xo;
+      if constexpr (VAR == TV_EDGE) {
+        if (c == 0) {                                         // column 0 (aligner.rs:98-104)
+          const bool rst = (t == lane);
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const int i = C.rowbase + k + 1;
+            S.Y[k] = rst ? 4 * wadd(col0_M(C.mode, i, a, C.b), a) + 2 : S.Y[k];
+          }
+          S.Xlast = rst ? S.Y[R - 1] - 1 : S.Xlast;
+        }
+        if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {    // column n2: M(i, n2)
+          if (lane == t - C.n2) {
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+              const int i = C.rowbase + k + 1;
+              if (i <= C.n1) C.lastcol[i] = (S.Y[k] >> 2) - a;
+            }
+          }
+        }
+      }
+      int out = S.Xlast;
+      if constexpr (VAR != TV_FAST) {
+#pragma unroll
+        for (int k = 0; k < R - 1; ++k) out = (C.orow == k) ? S.Y[k] - 1 : out;
+      }
+      C.oLane[u] = out;
+      // one step per scheduling region: hoisting later steps' profile lookups spills
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (h == 1 && c >= 1) {
+      // block c-1 (ring slots 0-63) is final: copy it out, slide the ring by one block
+      const int v = C.ring[lane];
+      const int nx = C.ring[64 + lane];
+      C.bndOut[(c - 1) * BG_CHUNK + lane] = v;
+      C.ring[lane] = nx;
+    } else if (h == 1) {
+      C.ring[lane] = C.ring[64 + lane];
+    }
+    // trace flush every 32 steps: block b, row k, lane r -> dwords [((b*R + k)*64 + r)*2, +2)
+    uint32_t* tb = C.trace + (size_t)((t0 >> 5) + h) * (R * 2 * BG_WAVE) + lane * 2;
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      *reinterpret_cast<uint2*>(tb + k * 2 * BG_WAVE) = make_uint2(S.tA[k], S.tB[k]);
+  }
+}
+
+}  // namespace
+
+// LDS layout (bytes from the dynamic base): lut 256 | progress counters 64 @prog_off |
+// code row @codes_off (64 bytes of slack before, 192 after) | per wave: 64-int boundary block +
+// 256-int ring @aux_lds_off.
+template <int R>
+__global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int lane = threadIdx.x & 63;
+  const int W = blockDim.x >> 6;
+  const int w = uni(threadIdx.x >> 6);
+  constexpr int ROWS = BG_WAVE * R;
+
+  if (threadIdx.x < 16) reinterpret_cast<int*>(smem + A.prog_off)[threadIdx.x] = 0;
+  uint8_t* sCodes = smem + A.codes_off;
+  {
+    const BgPair& Pp = A.pairs[blockIdx.x];
+    const uint8_t* g = A.codes2 + Pp.off2;
+    for (int x = threadIdx.x; x < Pp.n2; x += blockDim.x) sCodes[x] = g[x];
+  }
+  __syncthreads();
+
+  const BgPair P = A.pairs[blockIdx.x];
+  const int n1 = P.n1, n2 = P.n2, nst = P.nstrips, NC = P.nc;
+  if (nst == 0) return;
+  const int a = A.open;
+  const int b = A.ext;
+  const int mode = A.mode;
+  const size_t stripDw = (size_t)NC * (BG_CHUNK / BG_TRACE_BLK) * R * 2 * BG_WAVE;
+  int* waveLds = reinterpret_cast<int*>(smem + A.aux_lds_off) + w * (64 + 256);
+
+  TagCtx C;
+  C.a = a; C.b = b; C.mode = mode; C.n1 = n1; C.n2 = n2; C.lane = lane;
+  C.lastcol = A.aux + P.aux_off;
+  C.bIn = waveLds;
+  C.ring = waveLds + 64;
+
+  TagStrip<R> S;
+  const uint8_t* c1 = A.codes1 + P.off1;
+  const int nblk = NC - 1;
+  int* sProg = reinterpret_cast<int*>(smem + A.prog_off);
+  for (int s = w, rho = 0; s < nst; s += W, ++rho) {
+    C.rowbase = s * ROWS + lane * R;
+    const bool lastStrip = (s == nst - 1);
+    const int lastRow = n1 - 1 - s * ROWS;
+    const int olane = lastStrip ? lastRow / R : BG_WAVE - 1;
+    C.orow = lastStrip ? lastRow % R : R - 1;
+    const bool selRow = C.orow != R - 1;
+    C.oLane = C.ring + (lane <= olane ? 64 : 192) - lane;
+    C.trace = A.trace + P.trace_off / 4 + (size_t)s * stripDw;
+    C.bndOut = A.bndM + P.bnd_off + (size_t)s * NC * BG_CHUNK;
+    int qk[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int i = C.rowbase + k + 1;
+      qk[k] = c1[(i <= n1 ? i : n1) - 1];
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int i = C.rowbase + k + 1;
+      const int q = (i <= n1) ? qk[k] : 0;
+      S.prof[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];
+      S.Y[k] = 4 * wadd(col0_M(mode, i, a, b), a) + 2;
+      S.tA[k] = 0; S.tB[k] = 0;
+    }
+    S.topPrev = 0; S.Xlast = 1;
+    for (int c = 0; c < NC; ++c) {
+      // stage block c of the row above (X forms) for this wave
+      const int jb = c * BG_CHUNK + lane;
+      int bv;
+      if (s == 0) {
+        bv = 4 * wadd(row0_M(mode, jb, a, b), a) + 1;
+      } else {
+        if (c < nblk) {
+          const int need = ((s - 1) / W) * nblk + c + 1;
+          const int pw = (s - 1) % W;
+          while (__hip_atomic_load(sProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+            __builtin_amdgcn_s_sleep(1);
+        }
+        bv = load_agent(A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
+      }
+      waveLds[lane] = bv;
+      C.codeLane = sCodes + c * BG_CHUNK - lane - 1;
+      const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
+      if (edge) tag_chunk<R, TV_EDGE>(S, C, c);
+      else if (lastStrip && selRow) tag_chunk<R, TV_SEL>(S, C, c);
+      else tag_chunk<R, TV_FAST>(S, C, c);
+      // publish: the chunk ends with the block copy-out store and R trace stores; at vmcnt(R)
+      // the copy-out has reached L2
+      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
+      if (lane == 0)
+        __hip_atomic_store(sProg + w, rho * nblk + (c < nblk ? c : nblk), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+}
+
+template __global__ void bg_dp_tag_kernel<4>(BgDpArgs);
+template __global__ void bg_dp_tag_kernel<5>(BgDpArgs);
+template __global__ void bg_dp_tag_kernel<8>(BgDpArgs);
+template __global__ void bg_dp_tag_kernel<10>(BgDpArgs);
+
+extern "C" void* bg_dp_kernel_tag_ptr(int R) {
+  switch (R) {
+    case 4: return (void*)&bg_dp_tag_kernel<4>;
+    case 5: return (void*)&bg_dp_tag_kernel<5>;
+    case 8: return (void*)&bg_dp_tag_kernel<8>;
+    case 10: return (void*)&bg_dp_tag_kernel<10>;
+    default: return nullptr;
+  }
+}
