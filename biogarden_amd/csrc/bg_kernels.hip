@@ -508,7 +508,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   int k = ei, l = ej, state = 0, status = 0, ncore = 0;
   int curS = -1, curB0 = 0, curNb = 0;
   int k0 = -1000000, l0 = -1000000;                  // neighbourhood anchor (invalid)
-  int codes = 0, opacc = 0;
+  int codes = 0;
   // Transition table of backtrack (aligner.rs:520-586), per state, indexed by the 4-bit cell code
   // (bits 0-1 m_trace: 0 'R', 1 'X', 2 'Y', 3 STOP; bit 2 x_trace=='M'; bit 3 y_trace=='M').
   // Entry = (move << 2) | next state; move 0 none, 1 diag (op 0), 2 up (op 1), 3 left (op 2).
@@ -531,43 +531,96 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     for (int c = 0; c < 16; ++c) v |= (u64)((c & 8) ? 0 : ((3u << 2) | 2)) << (4 * c);
     return v;
   }();
+  // decodes the 8x8 neighbourhood anchored at (k, l): lane (dk, dl) holds cell (k - dk, l - dl)
+  auto reanchor = [&](int ka, int la) {
+    k0 = ka; l0 = la;
+    const int kk = k0 - (lane >> 3), ll = l0 - (lane & 7);
+    if (kk <= 0 || ll <= 0) {
+      codes = kCodeBorder | ((kk == 0) ? 2 : 1);    // m_trace borders: column 0 'X', row 0 'Y'
+    } else {
+      const int vr = kk - 1;
+      const int sidx = vr / ROWS, rem = vr - sidx * ROWS, r = rem / R, q = rem - r * R;
+      const int t = ll + r, bl = t >> 5;
+      if (sidx != curS || bl < curB0 || bl >= curB0 + curNb) {
+        codes = kCodeMiss;
+      } else {
+        const uint32_t* wp = win + (((bl - curB0) * R + q) * BG_WAVE + r) * NW;
+        const int bit = 31 - (t & 31);
+        int c;
+        if constexpr (AFFINE) {
+          const uint4 v = *reinterpret_cast<const uint4*>(wp);
+          c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | (((v.z >> bit) & 1) << 2) | (((v.w >> bit) & 1) << 3);
+        } else if (F.tag) {
+          const uint2 v = *reinterpret_cast<const uint2*>(wp);  // 2-bit codes, 16 steps/word
+          const int u = t & 31;
+          c = (int)(((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3) | 12;
+        } else {
+          const uint2 v = *reinterpret_cast<const uint2*>(wp);
+          c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | 12;
+        }
+        codes = c;
+      }
+    }
+  };
   for (;;) {
     int reqS = -1, reqB0 = 0, done = 0;
     if (wid == 0) {
       for (;;) {
         int dk = k0 - k, dl = l0 - l;
-        if ((unsigned)dk >= 8u || (unsigned)dl >= 8u) {
-          // re-anchor: lane (dk, dl) decodes cell (k - dk, l - dl)
-          k0 = k; l0 = l; dk = 0; dl = 0;
-          const int kk = k0 - (lane >> 3), ll = l0 - (lane & 7);
-          if (kk <= 0 || ll <= 0) {
-            codes = kCodeBorder | ((kk == 0) ? 2 : 1);  // m_trace borders: column 0 'X', row 0 'Y'
-          } else {
-            const int vr = kk - 1;
-            const int sidx = vr / ROWS, rem = vr - sidx * ROWS, r = rem / R, q = rem - r * R;
-            const int t = ll + r, bl = t >> 5;
-            if (sidx != curS || bl < curB0 || bl >= curB0 + curNb) {
-              codes = kCodeMiss;
-            } else {
-              const uint32_t* wp = win + (((bl - curB0) * R + q) * BG_WAVE + r) * NW;
-              const int bit = 31 - (t & 31);
-              int c;
-              if constexpr (AFFINE) {
-                const uint4 v = *reinterpret_cast<const uint4*>(wp);
-                c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | (((v.z >> bit) & 1) << 2) | (((v.w >> bit) & 1) << 3);
-              } else if (F.tag) {
-                const uint2 v = *reinterpret_cast<const uint2*>(wp);  // 2-bit codes, 16 steps/word
-                const int u = t & 31;
-                c = (int)(((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3) | 12;
-              } else {
-                const uint2 v = *reinterpret_cast<const uint2*>(wp);
-                c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | 12;
-              }
-              codes = c;
+        if ((unsigned)dk >= 8u || (unsigned)dl >= 8u) { reanchor(k, l); dk = 0; dl = 0; }
+        int c = rdlane(codes, dk * 8 + dl);
+        if constexpr (!AFFINE) {
+          // Linear gaps: inside the matrix x/y_trace are 'M', so states X/Y fall back to M
+          // without moving and the walk is a chain of m_trace moves.  Resolve the chain through
+          // the whole neighbourhood at once by pointer jumping (4 rounds of ds_bpermute over the
+          // 64 cells); the border, STOP and window-miss cells stay with the scalar walker below.
+          const bool jumpable = state == 0 && !(c & (kCodeMiss | kCodeBorder)) &&
+                                (MODE != BGK_LOCAL || (c & 3) != 3);
+          if (jumpable) {
+            if ((dk | dl) != 0) { reanchor(k, l); c = rdlane(codes, 0); }
+            const int cl = codes;
+            const bool term = (cl & (kCodeMiss | kCodeBorder)) || (MODE == BGK_LOCAL && (cl & 3) == 3);
+            const int mv = (int)(kLutM >> (4 * (cl & 15)) >> 2) & 3;   // 1 diag, 2 up, 3 left
+            const int nk = (lane >> 3) + (mv != 3), nl = (lane & 7) + (mv != 2);
+            const bool ex = !term && (nk >= 8 || nl >= 8);          // the move leaves the block
+            int p = (term || ex) ? lane : nk * 8 + nl;
+            int d = (term || ex) ? 0 : 1;
+            int J[4];
+            J[0] = p;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {                        // p <- p(p), d <- d + d(p)
+              const int qv = __builtin_amdgcn_ds_bpermute(p * 4, p | (d << 8));
+              p = qv & 255;
+              d += qv >> 8;
+              if (rr < 3) J[rr + 1] = p;
             }
+            // lane m finds the m-th cell of the chain from the anchor, then its move
+            int x = 0;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) {
+              const int y = __builtin_amdgcn_ds_bpermute(x * 4, J[bb]);
+              x = ((lane >> bb) & 1) ? y : x;
+            }
+            const int opx = __builtin_amdgcn_ds_bpermute(x * 4, mv - 1);
+            const int Pn = rdlane(p, 0), Dn = rdlane(d, 0);
+            const int infoP = rdlane((ex ? 1 : 0) | (mv << 1), Pn);
+            const int exP = infoP & 1, mvP = infoP >> 1;
+            const int nops = Dn + exP;
+            if (lane < nops) ob[cap - 1 - (ntail + ncore + lane)] = (uint8_t)opx;
+            ncore += nops;
+            k -= Pn >> 3;
+            l -= Pn & 7;
+            // state on arrival: after an up / left move the reference sits in X / Y, which only
+            // matters when the chain stopped on a border or window-miss cell
+            const int mvIn = exP ? mvP : (Dn > 0 ? rdlane(opx, Dn - 1) + 1 : 1);
+            if (exP) {
+              k -= (mvP != 3);
+              l -= (mvP != 2);
+            }
+            state = mvIn == 2 ? 1 : (mvIn == 3 ? 2 : 0);
+            continue;
           }
         }
-        const int c = rdlane(codes, dk * 8 + dl);
         if (c & kCodeMiss) {
           const int vr = k - 1;
           reqS = vr / ROWS;
@@ -590,8 +643,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         l -= (0xA >> mv) & 1;
         state = e & 3;
         if (mv) {
-          opacc = wrlane(mv - 1, ncore & 63, opacc);
-          if ((ncore & 63) == 63) ob[cap - 1 - (ntail + (ncore & ~63) + lane)] = (uint8_t)opacc;
+          if (lane == 0) ob[cap - 1 - (ntail + ncore)] = (uint8_t)(mv - 1);
           ++ncore;
         }
       }
@@ -626,7 +678,6 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     }
     __syncthreads();
   }
-  if (wid == 0 && lane < (ncore & 63)) ob[cap - 1 - (ntail + (ncore & ~63) + lane)] = (uint8_t)opacc;
 
   // ---------------- semiglobal prefix gaps (:416-428); every wave knows k, l through sh
   if (wid == 0 && lane == 0) { sh[7] = k; sh[8] = l; sh[9] = status; sh[10] = ncore; }

@@ -49,6 +49,34 @@ OPS(max3_f32, "v_max3_f32 %0, %0, %1, %2")
 OPS(pk_max_i16, "v_pk_max_i16 %0, %0, %1")
 OPS(pk_add_u16, "v_pk_add_u16 %0, %0, %1")
 
+OPS(add_sdwa, "v_add_u32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1")
+OPS(add_sdwa_w, "v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1")
+OPS(max_sdwa, "v_max_i32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2")
+OPS(mov_sdwa_pres, "v_mov_b32_sdwa %0, %1 dst_sel:BYTE_1 dst_unused:UNUSED_PRESERVE src0_sel:DWORD")
+OPS(add3_u32, "v_add3_u32 %0, %0, %1, %2")
+OPS(xor_b32, "v_xor_b32 %0, %0, %1")
+OPS(mov_b32, "v_mov_b32 %0, %1\n v_add_u32 %0, %0, %2")
+OPS(lshrrev, "v_lshrrev_b32 %0, %1, %0")
+OPS(ashrrev, "v_ashrrev_i32 %0, 2, %0")
+OPS(alignbit, "v_alignbit_b32 %0, %1, %0, 2")
+OPS(or3_b32, "v_or3_b32 %0, %0, %1, %2")
+OPS(and_or, "v_and_or_b32 %0, %0, %1, %2")
+OPS(cnd_e32, "v_cndmask_b32 %0, %0, %1, vcc")
+OPS(add_co, "v_add_co_u32 %0, vcc, %0, %1")
+OPS(sub_co, "v_sub_co_u32 %0, vcc, %0, %1")
+OPS(max_i16, "v_max_i16 %0, %0, %1")
+OPS(add_u16, "v_add_u16 %0, %0, %1")
+OPS(min_i32, "v_min_i32 %0, %0, %1")
+OPS(bfe_i32, "v_bfe_i32 %0, %1, %0, 8")
+OPS(add_k, "v_add_u32 %0, 0x1234, %0")
+OPS(and_k, "v_and_b32 %0, -4, %0")
+OPS(max_k, "v_max_i32 %0, 7, %0")
+OPS(sad_u8, "v_sad_u8 %0, %0, %1, %2")
+OPS(pk_max_i16x, "v_pk_max_i16 %0, %0, %1 op_sel_hi:[1,1]")
+OPS(mul_lo_u16, "v_mul_lo_u16 %0, %0, %1")
+OPS(max_f16, "v_max_f16 %0, %0, %1")
+OPS(add_f32, "v_add_f32 %0, %0, %1")
+
 typedef void (*kfn)(int*, int);
 static void run(const char* name, kfn f, int wavesPerCU) {
   int* d;
@@ -75,5 +103,8 @@ int main() {
   R(add_u32) R(and_b32) R(or_b32) R(sub_u32) R(lshlrev) R(max_i32) R(max_u32) R(max_f32) R(max3_i32)
   R(med3_i32) R(bfe_u32) R(perm_b32) R(mad_u24) R(lshl_add) R(cmp_e32) R(cmp_e64) R(addc_e32)
   R(addc_e64) R(cnd_e64) R(mov_dpp) R(add_dpp) R(readlane) R(max3_f32) R(pk_max_i16) R(pk_add_u16)
+  R(add_sdwa) R(add_sdwa_w) R(max_sdwa) R(mov_sdwa_pres) R(add3_u32) R(xor_b32) R(mov_b32) R(lshrrev)
+  R(ashrrev) R(alignbit) R(or3_b32) R(and_or) R(cnd_e32) R(add_co) R(sub_co) R(max_i16) R(add_u16)
+  R(min_i32) R(bfe_i32) R(add_k) R(and_k) R(max_k) R(sad_u8) R(pk_max_i16x) R(mul_lo_u16) R(max_f16) R(add_f32)
   return 0;
 }
