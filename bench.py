@@ -49,17 +49,23 @@ def cpu_baseline(pairs, mode, a, b, threads):
     return cells / secs / 1e9, secs, scores, sts
 
 
-def load_pmc_traffic(workload):
-    """HBM bytes per DP launch from the committed rocprofv3 PMC summary for this workload
-    (profiles/pmc_<workload>.json, written by tools/profile.sh), else None."""
+def load_pmc(workload):
+    """The committed rocprofv3 PMC summary for this workload (profiles/pmc_<workload>.json,
+    written by tools/pmc_traffic.py from tools/pmc.sh passes), else {}."""
     path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)
     if not os.path.exists(path):
-        return None
+        return {}
     try:
         with open(path) as f:
-            return json.load(f).get("hbm_bytes_per_launch")
+            return json.load(f)
     except (OSError, ValueError):
-        return None
+        return {}
+
+
+# Issue cost of the tagged kernel's cell (DESIGN.md "VALU issue ceiling"): 4 full-rate ops
+# (v_add/v_and, ~2.6 cycles per wave64 instruction per SIMD measured by tools/micro/valu_rates.hip)
+# + 3 half-rate ops (v_bfe, v_max3, v_alignbit, ~4.4 cycles) per 64 cells, 1024 SIMDs at 2.4 GHz.
+TAG_ISSUE_CELLS_PER_S = 64.0 / (4 * 2.6 + 3 * 4.4) * 1024 * 2.4e9
 
 
 def main():
@@ -80,6 +86,7 @@ def main():
     ap.add_argument("--cpu-pairs", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host timing")
     args = ap.parse_args()
 
     import torch
@@ -154,6 +161,20 @@ def main():
     else:
         results0 = [_native.decode_export(local.cpu().numpy().tobytes())]
 
+    # ---- host-to-host rate (not `value`): host buffers in, aligned strings back on the host
+    h2h = None
+    if not args.no_h2h:
+        h.set_pipeline(1)
+        torch.cuda.synchronize()
+        th = time.perf_counter()
+        h.prepare(args.mode, pairs, sc, args.open, args.extend)
+        h.execute()
+        h.fetch()
+        h2h_s = time.perf_counter() - th
+        h2h = {"gcups": round(cells / h2h_s / 1e9, 3), "seconds": round(h2h_s, 4),
+               "covers": "bg_batch_prepare (validation, residue coding, H2D) + execute + "
+                         "bg_batch_fetch (D2H of results and aligned strings), one call"}
+
     if rank != 0:
         if dist is not None:
             dist.destroy_process_group()
@@ -165,11 +186,22 @@ def main():
     bytes_per_cell = 0.25 if st["affine"] == 0 else 0.5
     algo_bytes = cells * bytes_per_cell + st["residue_bytes"]
     achieved = algo_bytes / (dp_ms * 1e-3) / 1e9 if dp_ms > 0 else 0.0
-    ops_per_cell = 10 if st["affine"] == 0 else 18
-    valu_achieved = ops_per_cell * cells / (dp_ms * 1e-3) if dp_ms > 0 else 0.0
     workload = "semiglobal_%dx%dx%d_blosum62_o%d_e%d" % (args.pairs, args.len1, args.len2,
                                                           -args.open, -args.extend)
-    traffic = load_pmc_traffic(workload)
+    pmc = load_pmc(workload)
+    same_geom = pmc.get("geometry") == [str(st["R"]), str(st["waves"])]
+    traffic = pmc.get("hbm_bytes_per_launch") if same_geom else None
+    cells_per_s = cells / (dp_ms * 1e-3) if dp_ms > 0 else 0.0
+    valu = {"lane_ops_peak": VALU_PEAK_OPS}
+    insts = pmc.get("raw_counters", {}).get("SQ_INSTS_VALU") if same_geom else None
+    if insts:
+        per_cell = insts * 64.0 / cells
+        valu.update({"instr_per_cell_measured": round(per_cell, 3),
+                     "lane_ops_achieved": per_cell * cells_per_s,
+                     "frac_of_lane_peak": round(per_cell * cells_per_s / VALU_PEAK_OPS, 4)})
+    if st["tagged"]:
+        valu.update({"issue_bound_cells_per_s": TAG_ISSUE_CELLS_PER_S,
+                     "frac_of_issue_bound": round(cells_per_s / TAG_ISSUE_CELLS_PER_S, 4)})
 
     # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0 only)
     cpu = None
@@ -203,18 +235,20 @@ def main():
                    "len2": args.len2, "mode": args.mode, "scoring": "blosum62",
                    "gap_open": args.open, "gap_extend": args.extend,
                    "kernel": {"R": st["R"], "waves": st["waves"], "affine": st["affine"],
-                              "dna_profile": st["dna"], "pipeline": args.pipeline},
+                              "tagged": st["tagged"], "dna_profile": st["dna"],
+                              "pipeline": args.pipeline},
                    "parallelism": "dp%d (independent pairs per rank)" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
                      "algorithmic_bytes_per_launch": int(algo_bytes),
+                     "traffic_source": ("profiles/pmc_%s.json" % workload) if traffic else None,
+                     "kernel": "bg_dp_tag_kernel" if st["tagged"] else "bg_dp_kernel",
                      "kernel_ms": round(dp_ms, 4), "finish_ms": round(fin_ms, 4),
-                     "valu": {"achieved_ops": valu_achieved, "peak_ops": VALU_PEAK_OPS,
-                              "frac": round(valu_achieved / VALU_PEAK_OPS, 4),
-                              "ops_per_cell_model": ops_per_cell}},
+                     "valu": valu},
         "cpu_baseline": cpu,
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+        "host_to_host": h2h,
         "all_status_ok": ok_status,
     }
     print(json.dumps(line))

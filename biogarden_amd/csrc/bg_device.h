@@ -70,7 +70,7 @@ struct BgDpArgs {
   int32_t* bndX;           // strip-boundary rows: X (affine kernels only)
   int32_t* aux;            // lastcol / rowbest / rowpos
   const int32_t* profile;  // DNA: [q] = 4 packed int8 S(q, c) - open; tagged kernel: [64+q] packed
-                           // 4(S-open)-1, [128+q] packed 4(S-open)-2; LDS path: int16 [32][32]
+                           // 4(S-2*open)-2, [128+q] packed 4(S-2*open)-3; LDS path: int16 [32][32]
   int32_t kdim;            // alphabet size (LDS path)
   int32_t open, ext;       // reference `a`, `b`
   int32_t mode;

@@ -313,13 +313,14 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   const double bound = ((double)maxAbsS + std::abs((double)a) + std::abs((double)b)) *
                        ((double)maxn1 + (double)maxn2 + 2.0);
   h->affine = (a >= b && bound < 1073741824.0) ? 0 : 1;
-  // tagged linear kernel: values 4(M+a)+tag must stay far from overflow, 4(S-a)-1/-2 fit int8
+  // tagged linear kernel: values 4(M - a(i+j)) + tag must stay far from overflow and the
+  // profile bytes 4(S-2a)-2 / -3 must fit int8
   bool tagOK = h->allowTag && !h->affine && mode != BG_LOCAL && dnaOK && bound < 134217728.0;
   for (int q = 0; q < 32 && tagOK; ++q)
     for (int c = 0; c < 32 && tagOK; ++c)
       if (present[q] && present[c]) {
-        const int64_t v = 4 * ((int64_t)sc->table[q * 32 + c] - (int64_t)a);
-        if (v - 2 < -128 || v - 1 > 127) tagOK = false;
+        const int64_t v = 4 * ((int64_t)sc->table[q * 32 + c] - 2 * (int64_t)a);
+        if (v - 3 < -128 || v - 2 > 127) tagOK = false;
       }
   h->tag = tagOK ? 1 : 0;
 
@@ -468,9 +469,9 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
         uint32_t px = 0, py = 0;
         for (int c = 0; c < 32; ++c) {
           if (dense[c] < 0) continue;
-          const int v = 4 * (sc->table[q * 32 + c] - a);
-          px |= (uint32_t)(uint8_t)(int8_t)(v - 1) << (8 * dense[c]);
-          py |= (uint32_t)(uint8_t)(int8_t)(v - 2) << (8 * dense[c]);
+          const int v = 4 * (sc->table[q * 32 + c] - 2 * a);   // frame M - a*(i+j)
+          px |= (uint32_t)(uint8_t)(int8_t)(v - 2) << (8 * dense[c]);
+          py |= (uint32_t)(uint8_t)(int8_t)(v - 3) << (8 * dense[c]);
         }
         prof[64 + dense[q]] = (int32_t)px;
         prof[128 + dense[q]] = (int32_t)py;

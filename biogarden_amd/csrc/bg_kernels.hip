@@ -379,7 +379,8 @@ __device__ __forceinline__ int lastrowM(const Fin& f, int j) {
   if (f.n1 == 0) return row0_M(f.mode, j, f.a, f.b);
   if (j == 0) return col0_M(f.mode, f.n1, f.a, f.b);
   const int v = f.lastrowMa[j];
-  return f.F->tag ? (v >> 2) - f.a : wadd(v, -f.a);    // tagged kernel stores 4(M+a)+1
+  // the tagged kernel stores X forms 4*(M(n1,j) - a*(n1+j)) + 2
+  return f.F->tag ? wadd(v >> 2, wmul(f.a, f.n1 + j)) : wadd(v, -f.a);
 }
 __device__ __forceinline__ int lastcolM(const Fin& f, int i) {
   if (f.n2 == 0) return col0_M(f.mode, i, f.a, f.b);
@@ -553,7 +554,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         } else if (F.tag) {
           const uint2 v = *reinterpret_cast<const uint2*>(wp);  // 2-bit codes, 16 steps/word
           const int u = t & 31;
-          c = (int)(((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3) | 12;
+          const int tg = (int)((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3;
+          c = ((0x2100 >> (4 * tg)) & 3) | 12;                 // tag 0 'R', 2 'X', 3 'Y'
         } else {
           const uint2 v = *reinterpret_cast<const uint2*>(wp);
           c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | 12;

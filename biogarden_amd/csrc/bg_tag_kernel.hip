@@ -6,9 +6,13 @@
 // of 64*R rows, lane r owns rows [rR, rR+R), anti-diagonal sweep with lane r at column t - r),
 // but everything per step that is not cell arithmetic is moved off the VALU:
 //
-//   * values are kept as 4*(M + a) + tag, tag 0 for the diagonal form, 1 for the X form (from
-//     the row above) and 2 for the Y form (from the left), so one v_max3 yields M and the
-//     m_trace code with the reference's tie priority Y > X > R (aligner.rs:455-463);
+//   * values live in the frame M'(i,j) = M(i,j) - a*(i+j), where both gap candidates carry no
+//     constant (M(i-1,j) + a and M(i,j-1) + a become M'(i-1,j) and M'(i,j-1)) and the diagonal
+//     one adds S - 2a (folded into the profile).  They are kept as 4*M' + tag with tag 0 for the
+//     diagonal form, 2 for the X form (from the row above) and 3 for the Y form (from the left),
+//     so one v_max3 yields M' and the m_trace code with the reference's tie priority
+//     Y > X > R (aligner.rs:455-463), the Y form of the result is `best | 3` and its X form
+//     `(best | 3) - 1`;
 //   * the column code is read by every lane from the pair's code row in LDS at (t - lane - 1)
 //     with a compile-time immediate offset per step (ds_read_u8, no VALU);
 //   * the row above of lane 0 (the boundary row of the strip above) is staged per 64-column
@@ -20,7 +24,7 @@
 //     below it write to a dummy half of the ring) — and each finished 64-column block is
 //     copied to HBM once per chunk.  No v_readlane / v_writelane in the loop.
 //
-// Per cell: v_bfe (profile byte), v_add, v_max3, v_alignbit (2-bit trace code), v_and, 2x v_add.
+// Per cell: v_bfe (profile byte), v_add, v_max3, v_alignbit (2-bit trace code), v_or, v_add.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,10 +36,10 @@ namespace {
 
 template <int R>
 struct TagStrip {
-  int Y[R];           // Y form of (i_k, j-1): 4*(M(i_k, j-1) + a) + 2
+  int Y[R];           // Y form of (i_k, j-1): 4*M'(i_k, j-1) + 3
   unsigned tA[R];     // trace codes of steps 0-15 of the current 32-step block (2 bits each)
   unsigned tB[R];     // steps 16-31
-  int prof[R];        // 4 packed int8: 4(S(q_k, c) - a) - 1 (row 0 of the lane) or - 2
+  int prof[R];        // 4 packed int8: 4(S(q_k, c) - 2a) - 2 (row 0 of the lane) or - 3
   int topPrev;        // X form of (row above, j-1) for the lane's first row
   int Xlast;          // X form of (lane's last row, j): handed down to lane r+1 by DPP
 };
@@ -53,10 +57,14 @@ struct TagCtx {
 
 enum { TV_FAST = 0, TV_SEL = 1, TV_EDGE = 2 };
 
+// Y form of column 0, row i: 4*(M(i,0) - a*i) + 3 (aligner.rs:98-104 borders)
+__device__ __forceinline__ int col0_Y(int mode, int i, int a, int b) {
+  return 4 * wadd(col0_M(mode, i, a, b), -wmul(a, i)) + 3;
+}
+
 template <int R, int VAR>
 __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c) {
   const int a = C.a;
-  const int a4x = 4 * a + 1;     // bm + a4x = X form, bm + a4x + 1 = Y form
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
   int nTop = C.bIn[0];
@@ -82,16 +90,16 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const int yo = S.Y[k];
-        const int d = dIn + sbfe(S.prof[k], code, 8);         // 4*(M(i-1,j-1) + S), tag 0
+        const int d = dIn + sbfe(S.prof[k], code, 8);         // 4*(M'(i-1,j-1) + S - 2a), tag 0
         const int best = imax(imax(d, xo), yo);
         // append the 2-bit code; the empty asm pins each update to its step (otherwise LLVM
         // sinks all 16 alignbits to the flush and keeps every step's `best` live)
         if (uu < 16) { S.tA[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tA[k], 2); asm volatile("" : "+v"(S.tA[k])); }
         else { S.tB[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tB[k], 2); asm volatile("" : "+v"(S.tB[k])); }
-        const int bm = best & ~3;                             // 4*M(i,j) - 4a
+        const int yn = best | 3;                              // Y form for column j+1
         dIn = yo;
-        xo = bm + a4x;                                        // X form for row i+1
-        S.Y[k] = bm + (a4x + 1);                              // Y form for column j+1
+        xo = yn - 1;                                          // X form for row i+1
+        S.Y[k] = yn;
       }
       S.topPrev = topX;
       S.Xlast = xo;
@@ -101,7 +109,7 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 #pragma unroll
           for (int k = 0; k < R; ++k) {
             const int i = C.rowbase + k + 1;
-            S.Y[k] = rst ? 4 * wadd(col0_M(C.mode, i, a, C.b), a) + 2 : S.Y[k];
+            S.Y[k] = rst ? col0_Y(C.mode, i, a, C.b) : S.Y[k];
           }
           S.Xlast = rst ? S.Y[R - 1] - 1 : S.Xlast;
         }
@@ -110,7 +118,7 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 #pragma unroll
             for (int k = 0; k < R; ++k) {
               const int i = C.rowbase + k + 1;
-              if (i <= C.n1) C.lastcol[i] = (S.Y[k] >> 2) - a;
+              if (i <= C.n1) C.lastcol[i] = wadd(S.Y[k] >> 2, wmul(a, i + C.n2));
             }
           }
         }
@@ -203,16 +211,16 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       const int i = C.rowbase + k + 1;
       const int q = (i <= n1) ? qk[k] : 0;
       S.prof[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];
-      S.Y[k] = 4 * wadd(col0_M(mode, i, a, b), a) + 2;
+      S.Y[k] = col0_Y(mode, i, a, b);
       S.tA[k] = 0; S.tB[k] = 0;
     }
-    S.topPrev = 0; S.Xlast = 1;
+    S.topPrev = 0; S.Xlast = 2;
     for (int c = 0; c < NC; ++c) {
       // stage block c of the row above (X forms) for this wave
       const int jb = c * BG_CHUNK + lane;
       int bv;
       if (s == 0) {
-        bv = 4 * wadd(row0_M(mode, jb, a, b), a) + 1;
+        bv = 4 * wadd(row0_M(mode, jb, a, b), -wmul(a, jb)) + 2;   // X form of row 0
       } else {
         if (c < nblk) {
           const int need = ((s - 1) / W) * nblk + c + 1;
