@@ -229,6 +229,79 @@ extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
     if ((x) != hipSuccess) return BG_E_HIP; \
   } while (0)
 
+// Geometry planner (DESIGN.md "Geometry").  For each strip height R and wave count W the strip
+// pipeline of the largest pair is simulated phase by phase (a phase = 64 anti-diagonal steps;
+// strip s starts two phases after strip s-1 and after its wave finished strip s-W).  A phase
+// with a active waves per SIMD costs 64 * ops_per_step * a * (4.0 + 0.6 / a) cycles: ~4 cycles
+// per VALU instruction when the SIMD is shared (tools/micro/tag_step.hip), a little more for a
+// lone wave.  Workgroups per CU are bounded by waves (32 per CU) and by VGPRs; with the two-slot
+// pipeline a finish workgroup must still fit beside them (one wave per SIMD).  Ties within 1 %
+// go to more waves per SIMD.
+static int vgprs_of(const void* fn) {
+  hipFuncAttributes at;
+  if (!fn || hipFuncGetAttributes(&at, fn) != hipSuccess || at.numRegs <= 0) return 128;
+  return (at.numRegs + 7) / 8 * 8;
+}
+
+static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncomp, int* Rout,
+                          int* Wout) {
+  const int cand[] = {4, 5, 8, 10};
+  const size_t np = std::max<size_t>(ncomp, 1);
+  const int NC = (int)(maxn2 / 64 + 2);
+  double best = 1e300;
+  int bestWps = 0;
+  std::vector<int> start, end, diff;
+  for (int Rc : cand) {
+    if (h->tuneR && Rc != h->tuneR) continue;
+    if (!bg_dp_has_R(Rc, h->affine, h->local, h->dna)) continue;
+    const void* fn = h->tag ? bg_dp_kernel_tag_ptr(Rc) : bg_dp_kernel_ptr(Rc, h->affine, h->local, h->dna);
+    const int vg = vgprs_of(fn);
+    const int fin = h->depth > 1 ? vgprs_of(bg_finish_kernel_ptr(Rc, h->affine, h->mode)) : 0;
+    const int opsPerStep = h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12);
+    const int S = maxn1 ? (int)((maxn1 + 64 * Rc - 1) / (64 * Rc)) : 1;
+    const int wmax = (h->affine || h->local) ? 8 : 16;
+    for (int Wc = 1; Wc <= wmax; ++Wc) {
+      if (h->tuneW && Wc != h->tuneW) continue;
+      if (Wc > S && !h->tuneW) continue;
+      const int wps = (Wc + 3) / 4;                      // waves per SIMD per workgroup
+      const int want = (int)((np + h->cus - 1) / h->cus);
+      int wg = std::min(want, 32 / Wc);
+      wg = std::min(wg, (512 - fin) / (wps * vg));
+      if (wg < 1) {
+        if (!(h->tuneR && h->tuneW)) continue;
+        wg = 1;
+      }
+      start.assign(S, 0);
+      end.assign(S, 0);
+      for (int s = 0; s < S; ++s) {
+        int st = s ? start[s - 1] + 2 : 0;
+        if (s >= Wc) st = std::max(st, end[s - Wc]);
+        start[s] = st;
+        end[s] = st + NC;
+      }
+      const int P = end[S - 1] > 0 ? *std::max_element(end.begin(), end.end()) : 0;
+      diff.assign(P + 1, 0);
+      for (int s = 0; s < S; ++s) { ++diff[start[s]]; --diff[end[s]]; }
+      double T = 0.0;
+      int A = 0;
+      for (int p = 0; p < P; ++p) {
+        A += diff[p];
+        const int a = std::max(1, (A * wg + 3) / 4);
+        T += 64.0 * opsPerStep * a * (4.0 + 0.6 / a);
+      }
+      const double rounds = std::ceil((double)np / ((double)h->cus * wg));
+      T *= rounds;
+      const int wpsAll = wps * wg;
+      if (T < best * 0.99 || (T < best * 1.01 && wpsAll > bestWps)) {
+        if (T < best) best = T;
+        *Rout = Rc;
+        *Wout = Wc;
+        bestWps = wpsAll;
+      }
+    }
+  }
+}
+
 extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
                                 const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                                 const bg_scoring* sc, int32_t a, int32_t b) {
@@ -325,37 +398,8 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   h->tag = tagOK ? 1 : 0;
 
   // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair).
-  // Cost model (DESIGN.md "Geometry"): a pair with S strips on W waves runs
-  //   phases = ((S-1)/W) * max(NC, 2W) + 2*((S-1) % W) + NC      chunks of 64 steps,
-  // each step costing ~(8R + 12) VALU issue slots per wave; a CU needs >= 2 waves per SIMD to
-  // fill its issue slots.  Pick the (R, W) with the least estimated time for the batch.
   int R = 8, W = 1;
-  {
-    const int cand[] = {4, 5, 8, 10};
-    double best = 1e300;
-    for (int Rc : cand) {
-      if (h->tuneR && Rc != h->tuneR) continue;
-      if (!bg_dp_has_R(Rc, h->affine, h->local, h->dna)) continue;
-      const size_t S = maxn1 ? (maxn1 + 64 * Rc - 1) / (64 * Rc) : 1;
-      const int wmax = (h->affine || h->local) ? 8 : 16;
-      for (int Wc = 1; Wc <= wmax; ++Wc) {
-        if (h->tuneW && Wc != h->tuneW) continue;
-        if ((size_t)Wc > S && !h->tuneW) continue;
-        const double NC = (double)(maxn2 / 64 + 2);
-        const double stride = std::max(NC, 2.0 * Wc);
-        const double phases = (double)((S - 1) / Wc) * stride + 2.0 * ((S - 1) % Wc) + NC;
-        // co-resident workgroups per CU (32 waves/CU), sequential rounds of workgroups
-        const double want = std::ceil((double)std::max<size_t>(ncomp, 1) / h->cus);
-        const double wgPerCu = std::max(1.0, std::min(want, std::floor(32.0 / Wc)));
-        const double rounds = std::ceil((double)std::max<size_t>(ncomp, 1) / (h->cus * wgPerCu));
-        // cycles between two instructions of one wave: a wave alone issues every 4 cycles, a
-        // SIMD every 2 cycles shared by its waves
-        const double period = std::max(4.0, 2.0 * Wc * wgPerCu / 4.0);
-        const double t = rounds * phases * 64.0 * (8.0 * Rc + 12.0) * period;
-        if (t < best) { best = t; R = Rc; W = Wc; }
-      }
-    }
-  }
+  plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
   size_t lds = 256;          // lut (+ int16 table and per-wave profiles on the LDS path)
   if (!h->dna) {
     const int WPE = (R + 1) / 2;
@@ -367,20 +411,30 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   }
   h->progOff = (int)lds;     // 16 per-wave progress counters follow
   lds += 64;
-  // seq2 codes staged in LDS when they fit next to the rest (160 KiB per CU)
   h->codesOff = (int)lds;
-  {
-    // the tagged kernel reads codes at (t - lane - 1) unclamped: 64 bytes of slack before the
-    // row (the counters/lut) and up to 127 after it
-    const size_t need = round_up(maxn2 + (h->tag ? 256 : 16), 16);
+  bool tagFits = false;
+  if (h->tag) {
+    // tagged kernel (bg_tag_kernel.hip): u16 scaled code row with 64 zero entries before it
+    // and (NC + 2) chunks in all, then per wave the boundary block, output ring and profile
+    // entries (4 codes x 64 lanes x RW dwords)
+    const int RW = R <= 4 ? 1 : (R <= 8 ? 2 : 4);
+    const size_t codes = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
+    const size_t waves = (size_t)W * (64 + 256 + 4 * 64 * RW) * 4;
+    tagFits = lds + codes + waves <= 160 * 1024;
+    if (tagFits) {
+      h->codesInLds = 1;
+      lds += codes;
+      h->auxLdsOff = (int)lds;
+      lds += waves;
+    }
+  }
+  if (!tagFits) {
+    h->tag = 0;
+    // seq2 codes staged in LDS when they fit next to the rest (160 KiB per CU)
+    const size_t need = round_up(maxn2 + 16, 16);
     h->codesInLds = (lds + need <= 160 * 1024) ? 1 : 0;
     if (h->codesInLds) lds += need;
-  }
-  h->auxLdsOff = (int)lds;
-  if (h->tag) {
-    const size_t ring = (size_t)W * (64 + 256) * 4;   // boundary block + output ring per wave
-    if (!h->codesInLds || lds + ring > 160 * 1024) h->tag = 0;
-    else lds += ring;
+    h->auxLdsOff = (int)lds;
   }
   h->R = R;
   h->W = W;

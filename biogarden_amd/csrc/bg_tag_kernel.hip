@@ -14,7 +14,10 @@
 //     Y > X > R (aligner.rs:455-463), the Y form of the result is `best | 3` and its X form
 //     `(best | 3) - 1`;
 //   * the column code is read by every lane from the pair's code row in LDS at (t - lane - 1)
-//     with a compile-time immediate offset per step (ds_read_u8, no VALU);
+//     with a compile-time immediate offset per step (ds_read_u16 of a pre-scaled code); it
+//     selects the lane's R profile bytes S'(q_k, code) from a per-wave LDS table (one ds_read
+//     per step) and each cell adds its byte with an SDWA operand select (v_add_u32_sdwa ...
+//     sext src1_sel:BYTE_k), so the profile lookup costs no VALU op of its own;
 //   * the row above of lane 0 (the boundary row of the strip above) is staged per 64-column
 //     block in LDS and read as a broadcast per step, feeding the `old` operand of the one DPP
 //     wave_shr:1 that moves each lane's last row down to the next lane;
@@ -24,7 +27,8 @@
 //     below it write to a dummy half of the ring) — and each finished 64-column block is
 //     copied to HBM once per chunk.  No v_readlane / v_writelane in the loop.
 //
-// Per cell: v_bfe (profile byte), v_add, v_max3, v_alignbit (2-bit trace code), v_or, v_add.
+// Per cell: v_add_sdwa (diagonal + profile byte), v_max3, v_alignbit (2-bit trace code), v_or,
+// v_add.  Per step: one DPP, one v_add (profile address).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -39,7 +43,6 @@ struct TagStrip {
   int Y[R];           // Y form of (i_k, j-1): 4*M'(i_k, j-1) + 3
   unsigned tA[R];     // trace codes of steps 0-15 of the current 32-step block (2 bits each)
   unsigned tB[R];     // steps 16-31
-  int prof[R];        // 4 packed int8: 4(S(q_k, c) - 2a) - 2 (row 0 of the lane) or - 3
   int topPrev;        // X form of (row above, j-1) for the lane's first row
   int Xlast;          // X form of (lane's last row, j): handed down to lane r+1 by DPP
 };
@@ -52,8 +55,37 @@ struct TagCtx {
   const int* bIn;           // LDS: staged boundary block of the strip above (64 X forms)
   int* ring;                // LDS: this wave's 256-slot output ring
   int* oLane;               // LDS: this lane's ring write base (slot = u + 64 - lane [+128])
-  const uint8_t* codeLane;  // LDS: code row + t0 - lane - 1 (this chunk)
+  const uint16_t* codeLane; // LDS: scaled code row + t0 - lane - 1 (this chunk)
+  const uint8_t* profLane;  // LDS: this lane's profile entries (+ scaled code = entry address)
 };
+
+// profile dwords per lane and code: R int8 bytes, padded to an aligned ds_read width
+template <int R>
+struct ProfW { static constexpr int v = R <= 4 ? 1 : (R <= 8 ? 2 : 4); };
+
+template <int RW>
+struct ProfV { int w[RW]; };
+
+template <int RW>
+__device__ __forceinline__ ProfV<RW> load_prof(const uint8_t* p) {
+  ProfV<RW> r;
+  if constexpr (RW == 1) {
+    r.w[0] = *reinterpret_cast<const int*>(p);
+  } else if constexpr (RW == 2) {
+    const int2 v = *reinterpret_cast<const int2*>(p);
+    r.w[0] = v.x; r.w[1] = v.y;
+  } else {
+    const int4 v = *reinterpret_cast<const int4*>(p);
+    r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
+  }
+  return r;
+}
+
+// x + sign_extend(byte `sel` of w): written as a constant-offset v_bfe_i32 + v_add, which the
+// SDWA peephole folds into one v_add_u32_sdwa ... sext src1_sel:BYTE_sel
+__device__ __forceinline__ int add_sbyte(int x, int w, int sel) {
+  return x + __builtin_amdgcn_sbfe(w, 8 * sel, 8);
+}
 
 enum { TV_FAST = 0, TV_SEL = 1, TV_EDGE = 2 };
 
@@ -67,30 +99,32 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
   const int a = C.a;
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
+  constexpr int RW = ProfW<R>::v;
+  // operand pipeline: the code of step u+2 and the profile entry of step u+1 are in flight
+  // while step u computes
   int nTop = C.bIn[0];
-  int nCode = C.codeLane[0];
+  ProfV<RW> nP = load_prof<RW>(C.profLane + C.codeLane[0]);
+  int nCode = C.codeLane[1];
+  const uint16_t* cl = C.codeLane + 2;   // advanced by 32 per half: immediate offsets inside
+  const int* bi = C.bIn + 1;
 #pragma unroll 1
-  for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h) {
+  for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h, cl += BG_TRACE_BLK, bi += BG_TRACE_BLK) {
 #pragma unroll
     for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
       const int u = h * BG_TRACE_BLK + uu;
       const int t = t0 + u;
       const int topIn = nTop;
-      const int code = nCode;
-      if (uu + 1 < BG_TRACE_BLK) {       // next step's operands are in flight during this one
-        nTop = C.bIn[u + 1];
-        nCode = C.codeLane[u + 1];
-      } else if (h == 0) {
-        nTop = C.bIn[BG_TRACE_BLK];
-        nCode = C.codeLane[BG_TRACE_BLK];
-      }
+      const ProfV<RW> P = nP;
+      nP = load_prof<RW>(C.profLane + nCode);
+      nCode = cl[uu];
+      nTop = bi[uu];
       const int topX = dpp_shr1(topIn, S.Xlast);             // X form of (row above, j)
       int dIn = S.topPrev;                                    // X form of (row above, j-1)
       int xo = topX;
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const int yo = S.Y[k];
-        const int d = dIn + sbfe(S.prof[k], code, 8);         // 4*(M'(i-1,j-1) + S - 2a), tag 0
+        const int d = add_sbyte(dIn, P.w[k >> 2], k & 3);      // 4*(M'(i-1,j-1) + S - 2a), tag 0
         const int best = imax(imax(d, xo), yo);
         // append the 2-bit code; the empty asm pins each update to its step (otherwise LLVM
         // sinks all 16 alignbits to the flush and keeps every step's `best` live)
@@ -151,9 +185,11 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 
 }  // namespace
 
-// LDS layout (bytes from the dynamic base): lut 256 | progress counters 64 @prog_off |
-// code row @codes_off (64 bytes of slack before, 192 after) | per wave: 64-int boundary block +
-// 256-int ring @aux_lds_off.
+// LDS layout (bytes from the dynamic base, offsets from the host, bg_tag_lds_bytes()):
+//   progress counters 64 B @prog_off | scaled code row @codes_off: u16, 64 zero entries, then
+//   (NC + 2) * 64 entries (code * 256 * RW, zero past n2) | per wave @aux_lds_off: 64-int
+//   boundary block, 256-int output ring, 4 codes x 64 lanes x RW-dword profile entries.
+constexpr int kTagWaveInts = 64 + 256;
 template <int R>
 __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -162,12 +198,15 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   const int w = uni(threadIdx.x >> 6);
   constexpr int ROWS = BG_WAVE * R;
 
+  constexpr int RW = ProfW<R>::v;
   if (threadIdx.x < 16) reinterpret_cast<int*>(smem + A.prog_off)[threadIdx.x] = 0;
-  uint8_t* sCodes = smem + A.codes_off;
+  uint16_t* sCodes = reinterpret_cast<uint16_t*>(smem + A.codes_off) + 64;
   {
     const BgPair& Pp = A.pairs[blockIdx.x];
-    const uint8_t* g = A.codes2 + Pp.off2;
-    for (int x = threadIdx.x; x < Pp.n2; x += blockDim.x) sCodes[x] = g[x];
+    const uint8_t* g = A.codes2 + Pp.off2;   // code * 8 (DNA path)
+    const int n = (Pp.nc + 2) * BG_CHUNK;
+    for (int x = (int)threadIdx.x - 64; x < n; x += blockDim.x)
+      sCodes[x] = (x >= 0 && x < Pp.n2) ? (uint16_t)(g[x] * (32 * RW)) : (uint16_t)0;
   }
   __syncthreads();
 
@@ -178,13 +217,15 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   const int b = A.ext;
   const int mode = A.mode;
   const size_t stripDw = (size_t)NC * (BG_CHUNK / BG_TRACE_BLK) * R * 2 * BG_WAVE;
-  int* waveLds = reinterpret_cast<int*>(smem + A.aux_lds_off) + w * (64 + 256);
+  int* waveLds = reinterpret_cast<int*>(smem + A.aux_lds_off) + w * (kTagWaveInts + 4 * 64 * RW);
+  int* profTab = waveLds + kTagWaveInts;
 
   TagCtx C;
   C.a = a; C.b = b; C.mode = mode; C.n1 = n1; C.n2 = n2; C.lane = lane;
   C.lastcol = A.aux + P.aux_off;
   C.bIn = waveLds;
   C.ring = waveLds + 64;
+  C.profLane = reinterpret_cast<const uint8_t*>(profTab + lane * RW);
 
   TagStrip<R> S;
   const uint8_t* c1 = A.codes1 + P.off1;
@@ -206,14 +247,26 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       const int i = C.rowbase + k + 1;
       qk[k] = c1[(i <= n1 ? i : n1) - 1];
     }
+    int pk[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       const int i = C.rowbase + k + 1;
       const int q = (i <= n1) ? qk[k] : 0;
-      S.prof[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];
+      pk[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];   // 4 codes x int8
       S.Y[k] = col0_Y(mode, i, a, b);
       S.tA[k] = 0; S.tB[k] = 0;
     }
+    // this lane's profile entries: for code cd, dword wd holds rows 4wd..4wd+3
+#pragma unroll
+    for (int cd = 0; cd < 4; ++cd)
+#pragma unroll
+      for (int wd = 0; wd < RW; ++wd) {
+        unsigned v = 0;
+#pragma unroll
+        for (int bb = 0; bb < 4; ++bb)
+          if (wd * 4 + bb < R) v |= (((unsigned)pk[wd * 4 + bb] >> (8 * cd)) & 0xffu) << (8 * bb);
+        profTab[(cd * 64 + lane) * RW + wd] = (int)v;
+      }
     S.topPrev = 0; S.Xlast = 2;
     for (int c = 0; c < NC; ++c) {
       // stage block c of the row above (X forms) for this wave
