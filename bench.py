@@ -62,10 +62,10 @@ def load_pmc(workload):
         return {}
 
 
-# Issue cost of the tagged kernel's cell (DESIGN.md "VALU issue ceiling"): 4 full-rate ops
-# (v_add/v_and, ~2.6 cycles per wave64 instruction per SIMD measured by tools/micro/valu_rates.hip)
-# + 3 half-rate ops (v_bfe, v_max3, v_alignbit, ~4.4 cycles) per 64 cells, 1024 SIMDs at 2.4 GHz.
-TAG_ISSUE_CELLS_PER_S = 64.0 / (4 * 2.6 + 3 * 4.4) * 1024 * 2.4e9
+# Register-only ceiling of the tagged kernel's step (tools/micro/tag_step.hip on MI355X, 16 waves
+# per CU, profiles/r01/micro_tag_step.txt): the same per-cell VALU sequence with no LDS, HBM,
+# strip pipeline or traceback.  DP cells/s by strip height R.
+TAG_REGISTER_CEILING = {4: 6.94e12, 5: 6.60e12, 8: 7.01e12, 10: 6.94e12}
 
 
 def main():
@@ -199,9 +199,10 @@ def main():
         valu.update({"instr_per_cell_measured": round(per_cell, 3),
                      "lane_ops_achieved": per_cell * cells_per_s,
                      "frac_of_lane_peak": round(per_cell * cells_per_s / VALU_PEAK_OPS, 4)})
-    if st["tagged"]:
-        valu.update({"issue_bound_cells_per_s": TAG_ISSUE_CELLS_PER_S,
-                     "frac_of_issue_bound": round(cells_per_s / TAG_ISSUE_CELLS_PER_S, 4)})
+    if st["tagged"] and st["R"] in TAG_REGISTER_CEILING:
+        ceil_ = TAG_REGISTER_CEILING[st["R"]]
+        valu.update({"register_ceiling_cells_per_s": ceil_,
+                     "frac_of_register_ceiling": round(cells_per_s / ceil_, 4)})
 
     # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0 only)
     cpu = None

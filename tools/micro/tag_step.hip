@@ -1,6 +1,7 @@
 // Microbenchmark: the tagged DP step (bg_tag_kernel.hip) on registers only — no LDS, no HBM,
 // no strip pipeline — to separate the cell arithmetic's own issue rate from everything else.
-// Per cell: v_bfe, v_add, v_max3, v_alignbit, v_and, 2x v_add; per step one DPP.
+// Per cell: v_add_u32_sdwa (diagonal + profile byte), v_max3, v_alignbit, v_or, v_add; per step
+// one DPP and one v_add per profile dword (stands in for the kernel's per-step ds_read).
 // ILP=2 interleaves two independent half-height strips in one wave.
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -11,7 +12,8 @@ __device__ __forceinline__ int dpp_shr1(int old, int src) {
 
 template <int R, int ILP>
 __global__ __launch_bounds__(1024) void tag_step(int* out, int iters, int a4x) {
-  int Y[ILP][R], prof[ILP][R];
+  constexpr int RW = (R + 3) / 4;
+  int Y[ILP][R], prof[ILP][RW];
   unsigned tA[ILP][R];
   int topPrev[ILP], Xlast[ILP];
 #pragma unroll
@@ -19,9 +21,10 @@ __global__ __launch_bounds__(1024) void tag_step(int* out, int iters, int a4x) {
 #pragma unroll
     for (int k = 0; k < R; ++k) {
       Y[g][k] = threadIdx.x * (k + 1) + g;
-      prof[g][k] = 0x01020304 * (k + 1 + g);
       tA[g][k] = 0;
     }
+#pragma unroll
+    for (int w = 0; w < RW; ++w) prof[g][w] = (int)(threadIdx.x * 0x01030507u) ^ (a4x * (w + 1 + g));
     topPrev[g] = 0;
     Xlast[g] = 1;
   }
@@ -29,37 +32,39 @@ __global__ __launch_bounds__(1024) void tag_step(int* out, int iters, int a4x) {
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      const int cd = code + u * 8;           // one v_add per step; 16 distinct lookups
 #pragma unroll
       for (int g = 0; g < ILP; ++g) {
+        int P[RW];
+#pragma unroll
+        for (int w = 0; w < RW; ++w) P[w] = prof[g][w] + code + u;
         const int topX = dpp_shr1(topPrev[g] + u, Xlast[g]);
         int dIn = topPrev[g];
         int xo = topX;
 #pragma unroll
         for (int k = 0; k < R; ++k) {
           const int yo = Y[g][k];
-          const int d = dIn + __builtin_amdgcn_sbfe(prof[g][k], cd, 8);
+          const int d = dIn + __builtin_amdgcn_sbfe(P[k >> 2], 8 * (k & 3), 8);
           const int best = __builtin_elementwise_max(__builtin_elementwise_max(d, xo), yo);
           tA[g][k] = __builtin_amdgcn_alignbit((unsigned)best, tA[g][k], 2);
           asm volatile("" : "+v"(tA[g][k]));
-          const int bm = best & ~3;
+          const int yn = best | 3;
           dIn = yo;
-          xo = bm + a4x;
-          Y[g][k] = bm + (a4x + 1);
+          xo = yn - 1;
+          Y[g][k] = yn;
         }
         topPrev[g] = topX;
         Xlast[g] = xo;
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    code = (code + 8) & 24;                  // keeps the profile lookups inside the loop
+    code = (code + 8) & 24;
   }
   int s = 0;
 #pragma unroll
   for (int g = 0; g < ILP; ++g)
 #pragma unroll
     for (int k = 0; k < R; ++k) s += Y[g][k] + (int)tA[g][k];
-  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s + a4x;
 }
 
 template <int R, int ILP>
@@ -79,7 +84,7 @@ void run(int wavesPerCU) {
   float ms;
   (void)hipEventElapsedTime(&ms, e0, e1);
   const double steps = (double)iters * 16 * ILP;             // per wave
-  const double instr = (double)iters * 16 * (ILP * (7.0 * R + 1) + 1);  // per wave
+  const double instr = (double)iters * 16 * ILP * (5.0 * R + 1 + (R + 3) / 4);  // per wave
   const double perSimd = instr * wavesPerCU / 4.0;
   const double cells = steps * R * 64 * wavesPerCU * 256.0;
   printf("R=%2d ILP=%d waves/CU=%2d  %.2f cycles per wave-instr per SIMD @2.4GHz   %.2f Tcells/s\n", R, ILP,
@@ -88,10 +93,9 @@ void run(int wavesPerCU) {
 }
 
 int main() {
-  for (int w : {4, 8, 16}) run<8, 1>(w);
-  for (int w : {4, 8, 16}) run<10, 1>(w);
-  for (int w : {4, 8, 16}) run<4, 2>(w);
-  for (int w : {4, 8}) run<8, 2>(w);
-  for (int w : {4, 8, 16}) run<5, 2>(w);
+  for (int w : {4, 8, 12, 16}) run<4, 1>(w);
+  for (int w : {4, 8, 12, 16}) run<5, 1>(w);
+  for (int w : {4, 8, 12, 16}) run<8, 1>(w);
+  for (int w : {4, 8, 12}) run<10, 1>(w);
   return 0;
 }
