@@ -144,20 +144,14 @@ def main():
     local = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     h.export_to(local.data_ptr(), nbytes)
     if dist is not None and not args.no_gather:
-        sizes = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([nbytes], dtype=torch.int64, device="cuda"))
-        mx = int(max(s.item() for s in sizes))
-        buf = torch.zeros(mx, dtype=torch.uint8, device="cuda")
-        buf[:nbytes] = local
+        from biogarden_amd import shard
         barrier()
         tg = time.perf_counter()
-        gl = [torch.empty(mx, dtype=torch.uint8, device="cuda") for _ in range(world)] if rank == 0 else None
-        dist.gather(buf, gl, dst=0)
+        packed = shard.gather_packed(local, dist, dst=0)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         if rank == 0:
-            results0 = [_native.decode_export(g[:int(s.item())].cpu().numpy().tobytes())
-                        for g, s in zip(gl, sizes)]
+            results0 = [_native.decode_export(b) for b in packed]
     else:
         results0 = [_native.decode_export(local.cpu().numpy().tobytes())]
 

@@ -65,14 +65,12 @@ class SequenceAligner:
         """Aligns many (seq1, seq2) pairs with one call.  Returns AlignmentResult per pair;
         with strict=True the first non-ok status raises like the single-pair methods."""
         pairs = [(_as_bytes(x), _as_bytes(y)) for x, y in pairs]
-        if isinstance(score, _score.ScoreTable):
-            sc = score.scoring()
-        else:
-            allb = b"".join(x + y for x, y in pairs)
-            sc = _score.tabulate(score, allb, b"")
+        sc, panics = _score.tabulate(score, pairs)
         out = self._h.align_batch(mode, pairs, sc, int(a), int(b))
         res = []
-        for r in out:
+        for (s1, s2), r in zip(pairs, out):
+            if r["status"] == 0 and _score.pair_panics(panics, s1, s2):
+                r = dict(r, status=_native.BG_UNSCORABLE)
             ar = AlignmentResult(r["score"], Sequence(r["aligned1"]), Sequence(r["aligned2"]),
                                  r["status"], r["end"], r["start"])
             if strict and r["status"]:
@@ -82,11 +80,10 @@ class SequenceAligner:
 
     def _one(self, mode, seq1, seq2, score, a, b):
         s1, s2 = _as_bytes(seq1), _as_bytes(seq2)
-        if isinstance(score, _score.ScoreTable):
-            sc = score.scoring()
-        else:
-            sc = _score.tabulate(score, s1, s2)
+        sc, panics = _score.tabulate(score, [(s1, s2)])
         r = self._h.align_batch(mode, [(s1, s2)], sc, int(a), int(b))[0]
+        if r["status"] == 0 and _score.pair_panics(panics, s1, s2):
+            r = dict(r, status=_native.BG_UNSCORABLE)
         res = (r["score"], Sequence(r["aligned1"]), Sequence(r["aligned2"]))
         _raise_for(r["status"], res)
         return res

@@ -42,29 +42,41 @@ pam250 = ScoreTable("pam250", _native.BG_PAM250)
 unit = ScoreTable("unit", _native.BG_UNIT)
 
 
-def tabulate(score, seq1, seq2):
+def tabulate(score, pairs):
     """A.8: turn an arbitrary closure S(byte1, byte2) into bg_scoring by calling it once per
-    distinct (byte of seq1, byte of seq2) pair.  A pair on which the closure raises is marked
-    unscorable (the reference would panic the first time the DP reached it)."""
+    distinct (byte of a seq1, byte of a seq2) pair of the batch.  Returns (scoring, panics):
+    `panics` is the set of (byte1, byte2) on which the closure raised; a pair whose
+    set(seq1) x set(seq2) meets it is one where the reference panics (status 3, see
+    pair_panics).  Built-in tables need no evaluation."""
     if isinstance(score, ScoreTable):
-        return score.scoring()
-    syms = sorted(set(bytes(seq1)) | set(bytes(seq2)))
+        return score.scoring(), set()
+    xs = set()
+    ys = set()
+    for s1, s2 in pairs:
+        xs.update(bytes(s1))
+        ys.update(bytes(s2))
+    syms = sorted(xs | ys)
     if len(syms) > 32:
         raise ValueError("more than 32 distinct symbols")
     sc = _native.BgScoring()
     sc.alphabet_size = len(syms)
     for x in range(256):
         sc.code[x] = 0xFF
-    bad = set()
     for i, x in enumerate(syms):
         sc.code[x] = i
-    for i, x in enumerate(syms):
-        for j, y in enumerate(syms):
+    panics = set()
+    for x in sorted(xs):
+        for y in sorted(ys):
             try:
-                sc.table[i * 32 + j] = int(score(x, y))
+                sc.table[sc.code[x] * 32 + sc.code[y]] = int(score(x, y))
             except Exception:
-                bad.add(x)
-                bad.add(y)
-    for x in bad:
-        sc.code[x] = 0xFF
-    return sc
+                panics.add((x, y))
+    return sc, panics
+
+
+def pair_panics(panics, seq1, seq2):
+    """True when the reference DP would evaluate a panicking (byte1, byte2) on this pair."""
+    if not panics or not seq1 or not seq2:
+        return False
+    a, b = set(bytes(seq1)), set(bytes(seq2))
+    return any(x in a and y in b for x, y in panics)

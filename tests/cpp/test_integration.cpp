@@ -1,0 +1,49 @@
+// The reference's alignment integration tests (tests/integration.rs:234-312) through the C++
+// facade on the GPU: same inputs, same calls, same expected scores and aligned strings.
+#include <cstdio>
+
+#include "biogarden.hpp"
+
+using namespace biogarden;
+
+int main(int argc, char** argv) {
+  const std::string fix = argc > 1 ? argv[1] : "tests/golden/reference_fixtures";
+  int fails = 0;
+  alignment::SequenceAligner aligner(0);   // SequenceAligner::new()
+  struct Case {
+    const char* name;
+    score::ScoreFn scoring;
+    int32_t a, b, expect;
+  } cases[] = {
+      {"global", score::blosum62, -11, -1, 232},
+      {"local", score::blosum62, -11, -1, 20431},
+      {"fitting", score::unit, -1, -1, 145},
+      {"overlap", score::unit, -2, -2, 698},
+      {"semiglobal", score::unit, -1, -1, 982},
+  };
+  for (auto& c : cases) {
+    auto inputs = io::fasta::read_tile(fix + "/input/" + c.name + "_alignment.fasta");
+    auto outputs = io::fasta::read_tile(fix + "/output/" + c.name + "_alignment.fasta");
+    const std::string n = c.name;
+    auto r = n == "global"    ? aligner.global_alignment(inputs[0], inputs[1], c.scoring, c.a, c.b)
+             : n == "local"   ? aligner.local_alignment(inputs[0], inputs[1], c.scoring, c.a, c.b)
+             : n == "fitting" ? aligner.fitting_alignment(inputs[0], inputs[1], c.scoring, c.a, c.b)
+             : n == "overlap" ? aligner.overlap_alignment(inputs[0], inputs[1], c.scoring, c.a, c.b)
+                              : aligner.semiglobal_alignment(inputs[0], inputs[1], c.scoring, c.a, c.b);
+    const auto& [score, s1, s2] = r.unwrap();
+    const bool ok = score == c.expect && s1 == outputs[0] && s2 == outputs[1];
+    std::printf("%-10s score %d (expect %d) %s\n", c.name, score, c.expect, ok ? "ok" : "MISMATCH");
+    fails += !ok;
+  }
+  // error behaviour (aligner.rs:87-89, 223-225)
+  auto e1 = aligner.global_alignment(ds::Sequence("ACGT"), ds::Sequence("ACG"), score::blosum62, 1, -1);
+  auto e2 = aligner.fitting_alignment(ds::Sequence("AC"), ds::Sequence("ACG"), score::unit, -1, -1);
+  fails += !(e1.is_err() && e1.error() == BioError::InvalidArgumentRange);
+  fails += !(e2.is_err() && e2.error() == BioError::InvalidInputSize);
+  bool panicked = false;
+  try { aligner.global_alignment(ds::Sequence("ACgT"), ds::Sequence("ACG"), score::blosum62, -1, -1); }
+  catch (const ReferencePanic&) { panicked = true; }
+  fails += !panicked;
+  std::printf("%s\n", fails ? "FAILED" : "integration ok");
+  return fails ? 1 : 0;
+}

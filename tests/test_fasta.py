@@ -53,3 +53,24 @@ def test_sequence_and_tile():
     assert str(s) == "ATGCA"
     t = Tile([Sequence("AC"), Sequence("G")])
     assert len(t) == 2 and t.size() == (2, 2) and t[1] == "G"
+
+
+def test_tabulate_closure_panics_per_pair():
+    """A.8: a closure is evaluated on set(seq1) x set(seq2) only; the pairs it panics on make
+    exactly the pairs whose DP would reach them unscorable."""
+    from biogarden_amd.alignment import score
+
+    def s(x, y):
+        if (x, y) == (ord("A"), ord("T")):
+            raise IndexError("panic")
+        return 2 if x == y else -1
+
+    sc, panics = score.tabulate(s, [(b"AC", b"GT"), (b"TT", b"AA")])
+    assert panics == {(ord("A"), ord("T"))}
+    assert sc.alphabet_size == 4
+    assert score.pair_panics(panics, b"AC", b"GT")
+    assert not score.pair_panics(panics, b"TT", b"AA")
+    assert not score.pair_panics(panics, b"", b"T")
+    assert sc.table[sc.code[ord("C")] * 32 + sc.code[ord("T")]] == -1
+    tab, none = score.tabulate(score.blosum62, [(b"AC", b"GT")])
+    assert none == set() and tab.alphabet_size == 26

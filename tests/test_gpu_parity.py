@@ -128,6 +128,30 @@ def test_custom_closure(aligner, oracle):
     assert st == 0 and got == (score, o1, o2)
 
 
+def test_closure_panics_only_where_reached(aligner, oracle):
+    """A closure that panics on one (byte1, byte2) makes exactly the pairs whose DP evaluates
+    it unscorable (status 3); the other pairs of the batch align normally (A.8)."""
+    from biogarden_amd.error import ReferencePanic
+
+    def total(x, y):
+        return 3 if x == y else -2
+
+    def partial(x, y):
+        if (x, y) == (ord("A"), ord("T")):
+            raise IndexError("score table index out of range")
+        return total(x, y)
+
+    pairs = [(b"ACGGA", b"GTTAC"), (b"CCGCG", b"GTAGG"), (b"TTATA", b"CCGCA")]
+    res = aligner.align_batch("global", pairs, partial, -4, -1)
+    assert [r.status for r in res] == [3, 0, 0]
+    sc = oracle.scoring(total)
+    for (s1, s2), r in list(zip(pairs, res))[1:]:
+        st, score, o1, o2 = oracle.align("global", s1, s2, sc, -4, -1, exact=True)
+        assert st == 0 and tuple(r[:3]) == (score, o1, o2)
+    with pytest.raises(ReferencePanic):
+        aligner.global_alignment(b"ACGGA", b"GTTAC", partial, -4, -1)
+
+
 # ------------------------------------------------------------------ seeded random vs oracle
 
 GAPS = [(-11, -1), (-2, -2), (-1, -2), (-3, -1), (0, 0), (-5, -5)]
