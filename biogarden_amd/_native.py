@@ -47,6 +47,7 @@ class BgStats(ctypes.Structure):
                 ("waves", ctypes.c_int32), ("affine", ctypes.c_int32), ("tagged", ctypes.c_int32),
                 ("dna", ctypes.c_int32),
                 ("local", ctypes.c_int32), ("npairs", ctypes.c_int32),
+                ("wide", ctypes.c_int32), ("workgroups", ctypes.c_int32),
                 ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float)]
 
 

@@ -29,6 +29,8 @@ struct BgPair {
   int32_t index;       // plan slot (results array index)
   uint64_t caller_off; // caller's output offset (sum of n1+n2 over earlier caller pairs)
   int32_t caller;      // caller's pair index
+  int32_t wg_count;    // tagged kernel, WIDE mode: workgroups working on this pair (else 1)
+  uint32_t prog_off;   // WIDE mode: offset of the pair's wg_count*W progress counters in gprog
   int32_t reserved;
 };
 
@@ -78,7 +80,9 @@ struct BgDpArgs {
   int32_t prog_off;        // byte offset of the 16 per-wave progress counters in dynamic LDS
   int32_t codes_off;       // byte offset of the staged seq2 codes in dynamic LDS
   int32_t codes_in_lds;    // 1 if every pair's seq2 fits there
-  int32_t aux_lds_off;     // tagged kernel: per-wave boundary block + output ring (1280 B/wave)
+  int32_t aux_lds_off;     // tagged kernel: per-wave area (boundary block, ring, profile, codes)
+  const int2* wgmap;       // tagged kernel, WIDE mode: per workgroup (plan index, index in group)
+  uint32_t* gprog;         // tagged kernel, WIDE mode: global per-wave progress counters
 };
 
 struct BgFinishArgs {

@@ -21,7 +21,8 @@
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
 extern "C" int bg_dp_has_R(int R, int affine, int local, int dna);
-extern "C" void* bg_dp_kernel_tag_ptr(int R);
+extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide);
+extern "C" int bg_dp_tag_wave_lds_bytes(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes();
 extern "C" void* bg_export_kernel_ptr();
@@ -98,6 +99,12 @@ struct bg_aligner {
   int codesOff = 320;
   int codesInLds = 0;
   int auxLdsOff = 0;
+  int wide = 0;                    // tagged kernel: pairs spread over groups of workgroups
+  std::vector<int> groupOf;        // caller pair -> workgroups (WIDE)
+  std::vector<int2> wgmap;
+  int gridWgs = 0;
+  uint32_t progWords = 0;
+  DevBuf wgmapBuf, gprogBuf;
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
   float dp_ms = 0.f, fin_ms = 0.f;
@@ -183,7 +190,8 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
-  for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs}) d->release();
+  for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs,
+                    &h->wgmapBuf, &h->gprogBuf}) d->release();
   for (Slot& S : h->slot) {
     for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results}) d->release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
@@ -199,7 +207,8 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
 }
 
 extern "C" int bg_set_tuning(bg_aligner* h, int R, int waves) {
-  if (!h || (R != 0 && R != 4 && R != 5 && R != 8 && R != 10) || waves < 0 || waves > 16) return BG_E_ARG;
+  if (!h || (R != 0 && R != 2 && R != 3 && R != 4 && R != 5 && R != 8 && R != 10) || waves < 0 || waves > 16)
+    return BG_E_ARG;
   h->tuneR = R;
   h->tuneW = waves;
   return BG_OK;
@@ -229,6 +238,62 @@ extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
     if ((x) != hipSuccess) return BG_E_HIP; \
   } while (0)
 
+// Strip pipeline of one pair on `gw` waves: phases (64-step chunks) until its last strip ends.
+static int pipeline_phases(int S, int gw, int NC) {
+  std::vector<int> start(S), end(S);
+  int P = 0;
+  for (int s = 0; s < S; ++s) {
+    int st = s ? start[s - 1] + 2 : 0;
+    if (s >= gw) st = std::max(st, end[s - gw]);
+    start[s] = st;
+    end[s] = st + NC;
+    P = std::max(P, end[s]);
+  }
+  return P;
+}
+
+// WIDE planner (tagged kernel, few large pairs): each pair gets a group of workgroups of 4 waves
+// (one wave per SIMD, a lone wave issues fastest) in proportion to its cells, at most one wave
+// per strip and at most the CU count in all, so every group is resident at once.  R minimises
+// the slowest pair's pipeline: phases * 64 steps * (5R + 2) ops * ~4.5 cycles.
+static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t npairs, int* Rout,
+                      int* Wout) {
+  std::vector<size_t> comp;
+  uint64_t cells = 0;
+  for (size_t p = 0; p < npairs; ++p)
+    if (h->prestatus[p] < 0 && n1[p] > 0 && n2[p] > 0) {
+      comp.push_back(p);
+      cells += (uint64_t)n1[p] * n2[p];
+    }
+  if (comp.empty() || comp.size() * 4 > (size_t)h->cus || h->tuneW) return false;
+  size_t maxn1 = 0;
+  for (size_t p : comp) maxn1 = std::max(maxn1, n1[p]);
+  if (maxn1 < 64 * 4 * 16) return false;                   // one workgroup's 16 waves suffice
+  const int W = 4;
+  const int cand[] = {2, 3, 4, 5, 8, 10};
+  double best = 1e300;
+  int bestR = 0;
+  std::vector<int> groups(npairs, 0), bestGroups;
+  for (int Rc : cand) {
+    if (h->tuneR && Rc != h->tuneR) continue;
+    double T = 0.0;
+    for (size_t p : comp) {
+      const int S = (int)((n1[p] + 64 * Rc - 1) / (64 * Rc));
+      const double share = (double)h->cus * ((double)n1[p] * n2[p]) / (double)cells;
+      int G = std::max(1, std::min((int)share, (S + W - 1) / W));
+      groups[p] = G;
+      const int NC = (int)(n2[p] / 64 + 2);
+      T = std::max(T, (double)pipeline_phases(S, G * W, NC) * 64.0 * (5 * Rc + 2) * 4.5);
+    }
+    if (T < best) { best = T; bestR = Rc; bestGroups = groups; }
+  }
+  if (!bestR) return false;
+  *Rout = bestR;
+  *Wout = W;
+  h->groupOf = bestGroups;
+  return true;
+}
+
 // Geometry planner (DESIGN.md "Geometry").  For each strip height R and wave count W the strip
 // pipeline of the largest pair is simulated phase by phase (a phase = 64 anti-diagonal steps;
 // strip s starts two phases after strip s-1 and after its wave finished strip s-W).  A phase
@@ -245,7 +310,7 @@ static int vgprs_of(const void* fn) {
 
 static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncomp, int* Rout,
                           int* Wout) {
-  const int cand[] = {4, 5, 8, 10};
+  const int cand[] = {2, 3, 4, 5, 8, 10};
   const size_t np = std::max<size_t>(ncomp, 1);
   const int NC = (int)(maxn2 / 64 + 2);
   double best = 1e300;
@@ -253,8 +318,8 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   std::vector<int> start, end, diff;
   for (int Rc : cand) {
     if (h->tuneR && Rc != h->tuneR) continue;
-    if (!bg_dp_has_R(Rc, h->affine, h->local, h->dna)) continue;
-    const void* fn = h->tag ? bg_dp_kernel_tag_ptr(Rc) : bg_dp_kernel_ptr(Rc, h->affine, h->local, h->dna);
+    if (!(h->tag ? bg_dp_kernel_tag_ptr(Rc, 0) != nullptr : bg_dp_has_R(Rc, h->affine, h->local, h->dna))) continue;
+    const void* fn = h->tag ? bg_dp_kernel_tag_ptr(Rc, 0) : bg_dp_kernel_ptr(Rc, h->affine, h->local, h->dna);
     const int vg = vgprs_of(fn);
     const int fin = h->depth > 1 ? vgprs_of(bg_finish_kernel_ptr(Rc, h->affine, h->mode)) : 0;
     const int opsPerStep = h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12);
@@ -267,6 +332,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
       const int want = (int)((np + h->cus - 1) / h->cus);
       int wg = std::min(want, 32 / Wc);
       wg = std::min(wg, (512 - fin) / (wps * vg));
+      if (h->tag) wg = std::min(wg, (int)(160 * 1024 / (64 + (size_t)Wc * bg_dp_tag_wave_lds_bytes(Rc))));
       if (wg < 1) {
         if (!(h->tuneR && h->tuneW)) continue;
         wg = 1;
@@ -397,39 +463,37 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
       }
   h->tag = tagOK ? 1 : 0;
 
-  // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair).
+  // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair, or a group
+  // of workgroups per pair in the tagged kernel's WIDE mode)
   int R = 8, W = 1;
-  plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
-  size_t lds = 256;          // lut (+ int16 table and per-wave profiles on the LDS path)
-  if (!h->dna) {
-    const int WPE = (R + 1) / 2;
-    for (;;) {
-      lds = 256 + 2048 + (size_t)W * h->kdim * 64 * WPE * 4;
-      if (lds + 64 <= 160 * 1024 || W == 1) break;
-      --W;
-    }
-  }
-  h->progOff = (int)lds;     // 16 per-wave progress counters follow
-  lds += 64;
-  h->codesOff = (int)lds;
-  bool tagFits = false;
+  h->wide = 0;
+  if (h->tag && plan_wide(h, n1, n2, npairs, &R, &W)) h->wide = 1;
+  else plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
+  size_t lds = 0;
   if (h->tag) {
-    // tagged kernel (bg_tag_kernel.hip): u16 scaled code row with 64 zero entries before it
-    // and (NC + 2) chunks in all, then per wave the boundary block, output ring and profile
-    // entries (4 codes x 64 lanes x RW dwords)
-    const int RW = R <= 4 ? 1 : (R <= 8 ? 2 : 4);
-    const size_t codes = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
-    const size_t waves = (size_t)W * (64 + 256 + 4 * 64 * RW) * 4;
-    tagFits = lds + codes + waves <= 160 * 1024;
-    if (tagFits) {
-      h->codesInLds = 1;
-      lds += codes;
-      h->auxLdsOff = (int)lds;
-      lds += waves;
+    // tagged kernel (bg_tag_kernel.hip): 16 progress counters, then per wave the boundary
+    // block, output ring, profile entries and the current chunk's codes
+    h->progOff = 0;
+    h->codesOff = 0;
+    h->codesInLds = 0;
+    h->auxLdsOff = 64;
+    lds = 64 + (size_t)W * bg_dp_tag_wave_lds_bytes(R);
+    // WIDE: one workgroup (one wave per SIMD) per CU — claim over half of the CU's LDS so the
+    // dispatcher cannot stack a group's workgroups on one CU
+    if (h->wide) lds = std::max<size_t>(lds, 80 * 1024 + 64);
+  } else {
+    lds = 256;               // lut (+ int16 table and per-wave profiles on the LDS path)
+    if (!h->dna) {
+      const int WPE = (R + 1) / 2;
+      for (;;) {
+        lds = 256 + 2048 + (size_t)W * h->kdim * 64 * WPE * 4;
+        if (lds + 64 <= 160 * 1024 || W == 1) break;
+        --W;
+      }
     }
-  }
-  if (!tagFits) {
-    h->tag = 0;
+    h->progOff = (int)lds;   // 16 per-wave progress counters follow
+    lds += 64;
+    h->codesOff = (int)lds;
     // seq2 codes staged in LDS when they fit next to the rest (160 KiB per CU)
     const size_t need = round_up(maxn2 + 16, 16);
     h->codesInLds = (lds + need <= 160 * 1024) ? 1 : 0;
@@ -450,6 +514,8 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   });
   h->plan.clear();
   h->plan.reserve(order.size());
+  h->wgmap.clear();
+  h->progWords = 0;
   uint64_t o1 = 0, o2 = 0, tro = 0, bo = 0, ao = 0, oo = 0;
   h->cells = 0;
   for (size_t p : order) {
@@ -474,6 +540,12 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     ao += round_up((uint64_t)(n1[p] + 1) + (h->local ? 2 * n1[p] : 0), 64);
     P.out_off = oo;
     oo += n1[p] + n2[p];
+    P.wg_count = h->wide ? std::max(1, h->groupOf[p]) : 1;
+    P.prog_off = h->wide ? h->progWords : 0;
+    if (h->wide) {
+      for (int g = 0; g < P.wg_count; ++g) h->wgmap.push_back(make_int2((int)h->plan.size(), g));
+      h->progWords += (uint32_t)(P.wg_count * W);
+    }
     h->cells += (uint64_t)n1[p] * n2[p];
     h->plan.push_back(P);
   }
@@ -484,8 +556,11 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   // ---- device memory
   if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->codes1.ensure(o1 + 16) ||
       !h->codes2.ensure(o2 + 16) || !h->lut.ensure(256) ||
-      !h->prof.ensure(2048) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)))
+      !h->prof.ensure(2048) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
+      !h->wgmapBuf.ensure(sizeof(int2) * (h->wgmap.size() + 1)) ||
+      !h->gprogBuf.ensure(4 * ((size_t)h->progWords + 1)))
     return BG_E_NOMEM;
+  h->gridWgs = h->wide ? (int)h->wgmap.size() : (int)h->plan.size();
   for (int z = 0; z < h->depth; ++z) {
     Slot& S = h->slot[z];
     if (!S.trace.ensure(tro + 256) || !S.bndM.ensure(bo * 4 + 256) ||
@@ -547,7 +622,10 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   BG_HIP(hipMemcpyAsync(h->lut.p, lut, 256, hipMemcpyHostToDevice, h->stream));
   BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), 2048, hipMemcpyHostToDevice, h->stream));
   if (!h->plan.empty())
-    BG_HIP(hipMemcpyAsync(h->pairs.p, h->plan.data(), sizeof(BgPair) * h->plan.size(),
+    if (h->wide)
+    BG_HIP(hipMemcpyAsync(h->wgmapBuf.p, h->wgmap.data(), sizeof(int2) * h->wgmap.size(),
+                          hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->pairs.p, h->plan.data(), sizeof(BgPair) * h->plan.size(),
                           hipMemcpyHostToDevice, h->stream));
   {
     std::vector<BgPairResultDev> tmpl(npairs);
@@ -583,7 +661,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[0], h->stream));
   if (np) {
-    void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R) : bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
+    void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide) : bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
     A.pairs = h->pairs.as<BgPair>();
@@ -596,6 +674,9 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.codes_off = h->codesOff;
     A.codes_in_lds = h->codesInLds;
     A.aux_lds_off = h->auxLdsOff;
+    A.wgmap = h->wgmapBuf.as<int2>();
+    A.gprog = h->gprogBuf.as<uint32_t>();
+    if (h->wide) BG_HIP(hipMemsetAsync(h->gprogBuf.p, 0, 4 * (size_t)h->progWords, h->stream));
     A.trace = S.trace.as<uint32_t>();
     A.bndM = S.bndM.as<int32_t>();
     A.bndX = S.bndX.as<int32_t>();
@@ -609,7 +690,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     void* args[] = {&A};
     if (h->lds > 65536)
       BG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds));
-    BG_HIP(hipLaunchKernel(fn, dim3(np), dim3(64 * h->W), args, h->lds, h->stream));
+    BG_HIP(hipLaunchKernel(fn, dim3(h->gridWgs), dim3(64 * h->W), args, h->lds, h->stream));
   }
   BG_HIP(hipEventRecord(e[1], h->stream));
   BG_HIP(hipEventRecord(S.dpDone, h->stream));
@@ -745,6 +826,8 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->R = h->R;
   o->waves = h->W;
   o->affine = h->affine;
+  o->wide = h->wide;
+  o->workgroups = h->gridWgs;
   o->tagged = h->tag;
   o->dna = h->dna;
   o->local = h->local;

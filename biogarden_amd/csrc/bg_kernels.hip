@@ -828,6 +828,8 @@ static void* finish_ptr(int mode) {
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode) {
   if (R == 4) return affine ? finish_ptr<4, true>(mode) : finish_ptr<4, false>(mode);
   if (R == 8) return affine ? finish_ptr<8, true>(mode) : finish_ptr<8, false>(mode);
+  if (R == 2 && !affine) return finish_ptr<2, false>(mode);
+  if (R == 3 && !affine) return finish_ptr<3, false>(mode);
   if (R == 5 && !affine) return finish_ptr<5, false>(mode);
   if (R == 10 && !affine) return finish_ptr<10, false>(mode);
   return nullptr;

@@ -55,7 +55,7 @@ struct TagCtx {
   const int* bIn;           // LDS: staged boundary block of the strip above (64 X forms)
   int* ring;                // LDS: this wave's 256-slot output ring
   int* oLane;               // LDS: this lane's ring write base (slot = u + 64 - lane [+128])
-  const uint16_t* codeLane; // LDS: scaled code row + t0 - lane - 1 (this chunk)
+  const uint16_t* codeLane; // LDS: this chunk's scaled codes, + u = column t0 + u - lane
   const uint8_t* profLane;  // LDS: this lane's profile entries (+ scaled code = entry address)
 };
 
@@ -94,7 +94,7 @@ __device__ __forceinline__ int col0_Y(int mode, int i, int a, int b) {
   return 4 * wadd(col0_M(mode, i, a, b), -wmul(a, i)) + 3;
 }
 
-template <int R, int VAR>
+template <int R, int VAR, bool WIDE>
 __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c) {
   const int a = C.a;
   const int t0 = c * BG_CHUNK;
@@ -170,7 +170,10 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
       // block c-1 (ring slots 0-63) is final: copy it out, slide the ring by one block
       const int v = C.ring[lane];
       const int nx = C.ring[64 + lane];
-      C.bndOut[(c - 1) * BG_CHUNK + lane] = v;
+      if constexpr (WIDE)   // read by workgroups on other XCDs: agent-coherent store
+        __hip_atomic_store(C.bndOut + (c - 1) * BG_CHUNK + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else
+        C.bndOut[(c - 1) * BG_CHUNK + lane] = v;
       C.ring[lane] = nx;
     } else if (h == 1) {
       C.ring[lane] = C.ring[64 + lane];
@@ -185,40 +188,56 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 
 }  // namespace
 
-// LDS layout (bytes from the dynamic base, offsets from the host, bg_tag_lds_bytes()):
-//   progress counters 64 B @prog_off | scaled code row @codes_off: u16, 64 zero entries, then
-//   (NC + 2) * 64 entries (code * 256 * RW, zero past n2) | per wave @aux_lds_off: 64-int
-//   boundary block, 256-int output ring, 4 codes x 64 lanes x RW-dword profile entries.
+// LDS layout (bytes from the dynamic base; the host sizes it in bg_host.cpp):
+//   16 progress counters (64 B, @prog_off; one-workgroup mode) | per wave @aux_lds_off:
+//   64-int boundary block, 256-int output ring, 4 codes x 64 lanes x RW-dword profile entries,
+//   192 u16 scaled codes of the current chunk (columns t0-64 .. t0+127).
+//
+// WIDE: the strips of one pair are spread over the pair's group of P.wg_count workgroups
+// (A.wgmap[blockIdx] = (pair, index in group)); strip s runs on the group's wave s mod (G*W)
+// and the progress counters live in global memory (A.gprog + P.prog_off), written and polled
+// with agent-scope atomics like the boundary rows, so the group may span XCDs.  All workgroups
+// of a group are resident together (the host caps the group at the CU count).
 constexpr int kTagWaveInts = 64 + 256;
+constexpr int kTagStageU16 = 192;
+
 template <int R>
+__host__ __device__ constexpr int tag_wave_ints() { return kTagWaveInts + 4 * 64 * ProfW<R>::v + kTagStageU16 / 2; }
+
+template <int R, bool WIDE>
 __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int RW = ProfW<R>::v;
   const int lane = threadIdx.x & 63;
   const int W = blockDim.x >> 6;
   const int w = uni(threadIdx.x >> 6);
   constexpr int ROWS = BG_WAVE * R;
 
-  constexpr int RW = ProfW<R>::v;
-  if (threadIdx.x < 16) reinterpret_cast<int*>(smem + A.prog_off)[threadIdx.x] = 0;
-  uint16_t* sCodes = reinterpret_cast<uint16_t*>(smem + A.codes_off) + 64;
-  {
-    const BgPair& Pp = A.pairs[blockIdx.x];
-    const uint8_t* g = A.codes2 + Pp.off2;   // code * 8 (DNA path)
-    const int n = (Pp.nc + 2) * BG_CHUNK;
-    for (int x = (int)threadIdx.x - 64; x < n; x += blockDim.x)
-      sCodes[x] = (x >= 0 && x < Pp.n2) ? (uint16_t)(g[x] * (32 * RW)) : (uint16_t)0;
+  int pairIdx = blockIdx.x, gi = 0;
+  if constexpr (WIDE) {
+    const int2 m = A.wgmap[blockIdx.x];
+    pairIdx = m.x;
+    gi = m.y;
   }
-  __syncthreads();
+  int* sProg = reinterpret_cast<int*>(smem + A.prog_off);
+  if constexpr (!WIDE) {
+    if (threadIdx.x < 16) sProg[threadIdx.x] = 0;
+    __syncthreads();
+  }
 
-  const BgPair P = A.pairs[blockIdx.x];
+  const BgPair P = A.pairs[pairIdx];
   const int n1 = P.n1, n2 = P.n2, nst = P.nstrips, NC = P.nc;
   if (nst == 0) return;
+  const int GW = (WIDE ? P.wg_count : 1) * W;                  // waves working on this pair
+  const int gw = gi * W + w;
+  uint32_t* gProg = WIDE ? A.gprog + P.prog_off : nullptr;
   const int a = A.open;
   const int b = A.ext;
   const int mode = A.mode;
   const size_t stripDw = (size_t)NC * (BG_CHUNK / BG_TRACE_BLK) * R * 2 * BG_WAVE;
-  int* waveLds = reinterpret_cast<int*>(smem + A.aux_lds_off) + w * (kTagWaveInts + 4 * 64 * RW);
+  int* waveLds = reinterpret_cast<int*>(smem + A.aux_lds_off) + w * tag_wave_ints<R>();
   int* profTab = waveLds + kTagWaveInts;
+  uint16_t* stage = reinterpret_cast<uint16_t*>(profTab + 4 * 64 * RW);
 
   TagCtx C;
   C.a = a; C.b = b; C.mode = mode; C.n1 = n1; C.n2 = n2; C.lane = lane;
@@ -226,12 +245,24 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   C.bIn = waveLds;
   C.ring = waveLds + 64;
   C.profLane = reinterpret_cast<const uint8_t*>(profTab + lane * RW);
+  C.codeLane = stage + 63 - lane;       // (t - lane - 1) - (t0 - 64) = u + 63 - lane
+
+  const uint8_t* c1 = A.codes1 + P.off1;
+  const uint8_t* g2 = A.codes2 + P.off2;  // code * 8 (DNA path)
+  // codes of columns t0-64+lane+64q, q = 0..2, scaled to profile-entry byte offsets
+  auto fetch_codes = [&](int c, int (&v)[3]) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int x = c * BG_CHUNK - 64 + lane + 64 * q;
+      const int xc = x < 0 ? 0 : (x >= n2 ? n2 - 1 : x);
+      const int cv = g2[xc];
+      v[q] = (x >= 0 && x < n2) ? cv * (32 * RW) : 0;
+    }
+  };
 
   TagStrip<R> S;
-  const uint8_t* c1 = A.codes1 + P.off1;
   const int nblk = NC - 1;
-  int* sProg = reinterpret_cast<int*>(smem + A.prog_off);
-  for (int s = w, rho = 0; s < nst; s += W, ++rho) {
+  for (int s = gw, rho = 0; s < nst; s += GW, ++rho) {
     C.rowbase = s * ROWS + lane * R;
     const bool lastStrip = (s == nst - 1);
     const int lastRow = n1 - 1 - s * ROWS;
@@ -268,7 +299,13 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         profTab[(cd * 64 + lane) * RW + wd] = (int)v;
       }
     S.topPrev = 0; S.Xlast = 2;
+    int cv[3];
+    fetch_codes(0, cv);
     for (int c = 0; c < NC; ++c) {
+      // this chunk's codes into LDS, the next chunk's in flight
+#pragma unroll
+      for (int q = 0; q < 3; ++q) stage[lane + 64 * q] = (uint16_t)cv[q];
+      if (c + 1 < NC) fetch_codes(c + 1, cv);
       // stage block c of the row above (X forms) for this wave
       const int jb = c * BG_CHUNK + lane;
       int bv;
@@ -276,40 +313,70 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         bv = 4 * wadd(row0_M(mode, jb, a, b), -wmul(a, jb)) + 2;   // X form of row 0
       } else {
         if (c < nblk) {
-          const int need = ((s - 1) / W) * nblk + c + 1;
-          const int pw = (s - 1) % W;
-          while (__hip_atomic_load(sProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-            __builtin_amdgcn_s_sleep(1);
+          const int need = ((s - 1) / GW) * nblk + c + 1;
+          const int pw = (s - 1) % GW;
+          if constexpr (WIDE) {
+            while ((int)__hip_atomic_load(gProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
+              __builtin_amdgcn_s_sleep(2);
+          } else {
+            while (__hip_atomic_load(sProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+              __builtin_amdgcn_s_sleep(1);
+          }
         }
         bv = load_agent(A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
       }
       waveLds[lane] = bv;
-      C.codeLane = sCodes + c * BG_CHUNK - lane - 1;
       const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
-      if (edge) tag_chunk<R, TV_EDGE>(S, C, c);
-      else if (lastStrip && selRow) tag_chunk<R, TV_SEL>(S, C, c);
-      else tag_chunk<R, TV_FAST>(S, C, c);
+      if (edge) tag_chunk<R, TV_EDGE, WIDE>(S, C, c);
+      else if (lastStrip && selRow) tag_chunk<R, TV_SEL, WIDE>(S, C, c);
+      else tag_chunk<R, TV_FAST, WIDE>(S, C, c);
       // publish: the chunk ends with the block copy-out store and R trace stores; at vmcnt(R)
-      // the copy-out has reached L2
+      // the copy-out has completed (vector memory operations complete in order)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
-      if (lane == 0)
-        __hip_atomic_store(sProg + w, rho * nblk + (c < nblk ? c : nblk), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int done = rho * nblk + (c < nblk ? c : nblk);
+      if constexpr (WIDE) {
+        if (lane == 0) __hip_atomic_store(gProg + gw, (uint32_t)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (lane == 0) __hip_atomic_store(sProg + w, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
   }
 }
 
-template __global__ void bg_dp_tag_kernel<4>(BgDpArgs);
-template __global__ void bg_dp_tag_kernel<5>(BgDpArgs);
-template __global__ void bg_dp_tag_kernel<8>(BgDpArgs);
-template __global__ void bg_dp_tag_kernel<10>(BgDpArgs);
+#define BG_TAG_INST(RR)                                            \
+  template __global__ void bg_dp_tag_kernel<RR, false>(BgDpArgs);  \
+  template __global__ void bg_dp_tag_kernel<RR, true>(BgDpArgs);
+BG_TAG_INST(2)
+BG_TAG_INST(3)
+BG_TAG_INST(4)
+BG_TAG_INST(5)
+BG_TAG_INST(8)
+BG_TAG_INST(10)
 
-extern "C" void* bg_dp_kernel_tag_ptr(int R) {
+extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide) {
   switch (R) {
-    case 4: return (void*)&bg_dp_tag_kernel<4>;
-    case 5: return (void*)&bg_dp_tag_kernel<5>;
-    case 8: return (void*)&bg_dp_tag_kernel<8>;
-    case 10: return (void*)&bg_dp_tag_kernel<10>;
+#define BG_TAG_CASE(RR) \
+    case RR: return wide ? (void*)&bg_dp_tag_kernel<RR, true> : (void*)&bg_dp_tag_kernel<RR, false>;
+    BG_TAG_CASE(2)
+    BG_TAG_CASE(3)
+    BG_TAG_CASE(4)
+    BG_TAG_CASE(5)
+    BG_TAG_CASE(8)
+    BG_TAG_CASE(10)
+#undef BG_TAG_CASE
     default: return nullptr;
+  }
+}
+
+// LDS bytes per wave of the tagged kernel (host sizing)
+extern "C" int bg_dp_tag_wave_lds_bytes(int R) {
+  switch (R) {
+    case 2: return tag_wave_ints<2>() * 4;
+    case 3: return tag_wave_ints<3>() * 4;
+    case 4: return tag_wave_ints<4>() * 4;
+    case 5: return tag_wave_ints<5>() * 4;
+    case 8: return tag_wave_ints<8>() * 4;
+    case 10: return tag_wave_ints<10>() * 4;
+    default: return 0;
   }
 }

@@ -130,6 +130,8 @@ typedef struct bg_stats {
   int32_t dna;             /* 1: register profile (<= 4 symbols), 0: LDS profile */
   int32_t local;
   int32_t npairs;
+  int32_t wide;            /* 1: tagged kernel with each pair spread over a group of workgroups */
+  int32_t workgroups;      /* DP grid size */
   float dp_ms;             /* last execute: DP kernel time (HIP events on the handle's stream) */
   float finish_ms;         /* last execute: end-cell + traceback kernel time */
 } bg_stats;
