@@ -100,6 +100,7 @@ struct bg_aligner {
   int codesInLds = 0;
   int auxLdsOff = 0;
   int wide = 0;                    // tagged kernel: pairs spread over groups of workgroups
+  int tagRow = 0;                  // tagged kernel: the code row staged whole in LDS
   std::vector<int> groupOf;        // caller pair -> workgroups (WIDE)
   std::vector<int2> wgmap;
   int gridWgs = 0;
@@ -291,6 +292,7 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
   *Rout = bestR;
   *Wout = W;
   h->groupOf = bestGroups;
+  h->tagRow = 1;                   // kept when it fits (the LDS is padded to one group per CU)
   return true;
 }
 
@@ -331,8 +333,20 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
       const int wps = (Wc + 3) / 4;                      // waves per SIMD per workgroup
       const int want = (int)((np + h->cus - 1) / h->cus);
       int wg = std::min(want, 32 / Wc);
-      wg = std::min(wg, (512 - fin) / (wps * vg));
-      if (h->tag) wg = std::min(wg, (int)(160 * 1024 / (64 + (size_t)Wc * bg_dp_tag_wave_lds_bytes(Rc))));
+      // VGPRs: a workgroup's waves spread over the 4 SIMDs; each SIMD keeps room for one
+      // traceback wave when pipelining
+      if (Wc >= 4) wg = std::min(wg, (512 - fin) / (wps * vg));
+      else wg = std::min(wg, 4 * ((512 - fin) / vg) / Wc);
+      bool rowc = false;
+      if (h->tag) {
+        // the code row in LDS saves per-chunk staging, unless it costs co-resident workgroups
+        const size_t waves = (size_t)Wc * bg_dp_tag_wave_lds_bytes(Rc);
+        const size_t row = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
+        const int wgNoRow = (int)(160 * 1024 / (128 + waves));
+        const int wgRow = (int)(160 * 1024 / (128 + waves + row));
+        rowc = wgRow >= std::min(wg, wgNoRow) && wgRow >= 1;
+        wg = std::min(wg, rowc ? wgRow : wgNoRow);
+      }
       if (wg < 1) {
         if (!(h->tuneR && h->tuneW)) continue;
         wg = 1;
@@ -363,6 +377,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
         *Rout = Rc;
         *Wout = Wc;
         bestWps = wpsAll;
+        h->tagRow = rowc ? 1 : 0;
       }
     }
   }
@@ -471,13 +486,15 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   else plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
   size_t lds = 0;
   if (h->tag) {
-    // tagged kernel (bg_tag_kernel.hip): 16 progress counters, then per wave the boundary
-    // block, output ring, profile entries and the current chunk's codes
+    // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
+    // boundary block, output ring, profile entries, the current chunk's codes and the mailbox
     h->progOff = 0;
-    h->codesOff = 0;
-    h->codesInLds = 0;
-    h->auxLdsOff = 64;
-    lds = 64 + (size_t)W * bg_dp_tag_wave_lds_bytes(R);
+    h->codesOff = 128;
+    const size_t waves = (size_t)W * bg_dp_tag_wave_lds_bytes(R);
+    const size_t row = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
+    h->codesInLds = (h->tagRow && 128 + row + waves <= 160 * 1024) ? 1 : 0;
+    h->auxLdsOff = (int)(128 + (h->codesInLds ? row : 0));
+    lds = h->auxLdsOff + waves;
     // WIDE: one workgroup (one wave per SIMD) per CU — claim over half of the CU's LDS so the
     // dispatcher cannot stack a group's workgroups on one CU
     if (h->wide) lds = std::max<size_t>(lds, 80 * 1024 + 64);

@@ -56,6 +56,8 @@ struct TagCtx {
   int* ring;                // LDS: this wave's 256-slot output ring
   int* oLane;               // LDS: this lane's ring write base (slot = u + 64 - lane [+128])
   const uint16_t* codeLane; // LDS: this chunk's scaled codes, + u = column t0 + u - lane
+  int* mail;                // LDS mailbox slot for the block finished in this chunk (consumer
+                            // in this workgroup), or nullptr: the block goes to HBM
   const uint8_t* profLane;  // LDS: this lane's profile entries (+ scaled code = entry address)
 };
 
@@ -170,7 +172,9 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
       // block c-1 (ring slots 0-63) is final: copy it out, slide the ring by one block
       const int v = C.ring[lane];
       const int nx = C.ring[64 + lane];
-      if constexpr (WIDE)   // read by workgroups on other XCDs: agent-coherent store
+      if (C.mail)           // the next strip runs on a wave of this workgroup
+        C.mail[lane] = v;
+      else if constexpr (WIDE)   // read by workgroups on other XCDs: agent-coherent store
         __hip_atomic_store(C.bndOut + (c - 1) * BG_CHUNK + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
         C.bndOut[(c - 1) * BG_CHUNK + lane] = v;
@@ -189,9 +193,15 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 }  // namespace
 
 // LDS layout (bytes from the dynamic base; the host sizes it in bg_host.cpp):
-//   16 progress counters (64 B, @prog_off; one-workgroup mode) | per wave @aux_lds_off:
-//   64-int boundary block, 256-int output ring, 4 codes x 64 lanes x RW-dword profile entries,
-//   192 u16 scaled codes of the current chunk (columns t0-64 .. t0+127).
+//   16 produced + 16 consumed counters (128 B, @prog_off) | the pair's scaled code row when it
+//   fits (@codes_off, u16, 64 zeros before it, NC + 2 chunks) | per wave @aux_lds_off: 64-int
+//   boundary block, 256-int output ring, 4 codes x 64 lanes x RW-dword profile entries, 192 u16
+//   scaled codes of the current chunk (columns t0-64 .. t0+127), 4 x 64-int mailbox.
+//
+// Boundary rows between strips on two waves of the same workgroup go through the producer's
+// LDS mailbox (slot = block sequence number mod 4, flow-controlled by the consumer's counter),
+// never through HBM; only a strip whose successor starts a new round (or sits in another
+// workgroup, or is the finish kernel) writes its row to HBM.
 //
 // WIDE: the strips of one pair are spread over the pair's group of P.wg_count workgroups
 // (A.wgmap[blockIdx] = (pair, index in group)); strip s runs on the group's wave s mod (G*W)
@@ -200,9 +210,12 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 // of a group are resident together (the host caps the group at the CU count).
 constexpr int kTagWaveInts = 64 + 256;
 constexpr int kTagStageU16 = 192;
+constexpr int kMailSlots = 4;   // boundary blocks in flight between two waves of a workgroup
 
 template <int R>
-__host__ __device__ constexpr int tag_wave_ints() { return kTagWaveInts + 4 * 64 * ProfW<R>::v + kTagStageU16 / 2; }
+__host__ __device__ constexpr int tag_wave_ints() {
+  return kTagWaveInts + 4 * 64 * ProfW<R>::v + kTagStageU16 / 2 + kMailSlots * 64;
+}
 
 template <int R, bool WIDE>
 __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
@@ -219,11 +232,20 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     pairIdx = m.x;
     gi = m.y;
   }
-  int* sProg = reinterpret_cast<int*>(smem + A.prog_off);
-  if constexpr (!WIDE) {
-    if (threadIdx.x < 16) sProg[threadIdx.x] = 0;
-    __syncthreads();
+  int* sProg = reinterpret_cast<int*>(smem + A.prog_off);   // blocks produced (per wave)
+  int* sCons = sProg + 16;                                   // chunks consumed (per wave)
+  if (threadIdx.x < 32) sProg[threadIdx.x] = 0;
+  // the pair's whole scaled code row, when it fits (A.codes_in_lds): 64 zero entries before it
+  // and zeros past n2 up to (NC + 2) chunks; else codes are staged per wave and chunk
+  uint16_t* sRow = reinterpret_cast<uint16_t*>(smem + A.codes_off) + 64;
+  if (A.codes_in_lds) {
+    const BgPair& Pp = A.pairs[pairIdx];
+    const uint8_t* g = A.codes2 + Pp.off2;
+    const int n = (Pp.nc + 2) * BG_CHUNK;
+    for (int x = (int)threadIdx.x - 64; x < n; x += blockDim.x)
+      sRow[x] = (x >= 0 && x < Pp.n2) ? (uint16_t)(g[x] * (32 * RW)) : (uint16_t)0;
   }
+  __syncthreads();
 
   const BgPair P = A.pairs[pairIdx];
   const int n1 = P.n1, n2 = P.n2, nst = P.nstrips, NC = P.nc;
@@ -238,25 +260,38 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   int* waveLds = reinterpret_cast<int*>(smem + A.aux_lds_off) + w * tag_wave_ints<R>();
   int* profTab = waveLds + kTagWaveInts;
   uint16_t* stage = reinterpret_cast<uint16_t*>(profTab + 4 * 64 * RW);
+  int* mailbox = profTab + 4 * 64 * RW + kTagStageU16 / 2;   // this wave's outgoing blocks
+  const int prevW = (w + W - 1) % W;                         // producer wave of the strip above
+  int* prevMail = reinterpret_cast<int*>(smem + A.aux_lds_off) + prevW * tag_wave_ints<R>() +
+                  (kTagWaveInts + 4 * 64 * RW + kTagStageU16 / 2);
 
   TagCtx C;
   C.a = a; C.b = b; C.mode = mode; C.n1 = n1; C.n2 = n2; C.lane = lane;
   C.lastcol = A.aux + P.aux_off;
   C.bIn = waveLds;
+  C.mail = nullptr;
   C.ring = waveLds + 64;
   C.profLane = reinterpret_cast<const uint8_t*>(profTab + lane * RW);
+  const bool rowInLds = A.codes_in_lds != 0;
   C.codeLane = stage + 63 - lane;       // (t - lane - 1) - (t0 - 64) = u + 63 - lane
 
   const uint8_t* c1 = A.codes1 + P.off1;
   const uint8_t* g2 = A.codes2 + P.off2;  // code * 8 (DNA path)
-  // codes of columns t0-64+lane+64q, q = 0..2, scaled to profile-entry byte offsets
+  // raw codes of columns t0-64+lane+64q, q = 0..2 (clamped, unconditional loads: they are only
+  // consumed at the next chunk's start, so their latency hides behind a whole chunk)
   auto fetch_codes = [&](int c, int (&v)[3]) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const int x = c * BG_CHUNK - 64 + lane + 64 * q;
-      const int xc = x < 0 ? 0 : (x >= n2 ? n2 - 1 : x);
-      const int cv = g2[xc];
-      v[q] = (x >= 0 && x < n2) ? cv * (32 * RW) : 0;
+      v[q] = g2[x < 0 ? 0 : (x >= n2 ? n2 - 1 : x)];
+    }
+  };
+  // ... scaled to profile-entry byte offsets (0 outside the row) when staged
+  auto stage_codes = [&](int c, const int (&v)[3]) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int x = c * BG_CHUNK - 64 + lane + 64 * q;
+      stage[lane + 64 * q] = (uint16_t)(((unsigned)x < (unsigned)n2) ? v[q] * (32 * RW) : 0);
     }
   };
 
@@ -272,6 +307,10 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     C.oLane = C.ring + (lane <= olane ? 64 : 192) - lane;
     C.trace = A.trace + P.trace_off / 4 + (size_t)s * stripDw;
     C.bndOut = A.bndM + P.bnd_off + (size_t)s * NC * BG_CHUNK;
+    // strip s+1 on the next wave of this workgroup in this round: hand blocks over in LDS
+    const bool mailOut = (s + 1 < nst) && (w + 1 < W);
+    // strip s-1 on the previous wave of this workgroup in this round: read its mailbox
+    const bool mailIn = (s > 0) && (w > 0);
     int qk[R];
 #pragma unroll
     for (int k = 0; k < R; ++k) {
@@ -299,46 +338,70 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         profTab[(cd * 64 + lane) * RW + wd] = (int)v;
       }
     S.topPrev = 0; S.Xlast = 2;
-    int cv[3];
-    fetch_codes(0, cv);
+    int cv[3] = {0, 0, 0};
+    if (!rowInLds) fetch_codes(0, cv);
     for (int c = 0; c < NC; ++c) {
-      // this chunk's codes into LDS, the next chunk's in flight
-#pragma unroll
-      for (int q = 0; q < 3; ++q) stage[lane + 64 * q] = (uint16_t)cv[q];
-      if (c + 1 < NC) fetch_codes(c + 1, cv);
-      // stage block c of the row above (X forms) for this wave
+      if (rowInLds) {
+        C.codeLane = sRow + c * BG_CHUNK - lane - 1;
+      } else {
+        // this chunk's codes into LDS, the next chunk's in flight
+        stage_codes(c, cv);
+        fetch_codes(c + 1 < NC ? c + 1 : c, cv);
+      }
+      // the row above, block c: row 0, the producer's LDS mailbox, or HBM
+      const int seq = rho * NC + c;                              // block sequence number
       const int jb = c * BG_CHUNK + lane;
-      int bv;
       if (s == 0) {
-        bv = 4 * wadd(row0_M(mode, jb, a, b), -wmul(a, jb)) + 2;   // X form of row 0
+        waveLds[lane] = 4 * wadd(row0_M(mode, jb, a, b), -wmul(a, jb)) + 2;   // X form of row 0
+        C.bIn = waveLds;
       } else {
         if (c < nblk) {
           const int need = ((s - 1) / GW) * nblk + c + 1;
-          const int pw = (s - 1) % GW;
-          if constexpr (WIDE) {
+          const int pw = mailIn ? prevW : (s - 1) % GW;
+          if (WIDE && !mailIn) {
             while ((int)__hip_atomic_load(gProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
               __builtin_amdgcn_s_sleep(2);
           } else {
-            while (__hip_atomic_load(sProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+            while (__hip_atomic_load(sProg + pw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
               __builtin_amdgcn_s_sleep(1);
           }
         }
-        bv = load_agent(A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
+        if (mailIn) {
+          C.bIn = prevMail + (seq % kMailSlots) * 64;
+        } else {
+          waveLds[lane] = load_agent(A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
+          C.bIn = waveLds;
+        }
       }
-      waveLds[lane] = bv;
+      // the block this chunk finishes (c-1) goes to mailbox slot (seq-1) mod 4 once the
+      // consumer has finished the chunk that read that slot last (sequence seq-1-4)
+      C.mail = nullptr;
+      if (mailOut && c >= 1 && c - 1 < nblk) {
+        const int needC = seq - kMailSlots;                      // consumer chunks finished
+        while (__hip_atomic_load(sCons + w + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < needC)
+          __builtin_amdgcn_s_sleep(1);
+        C.mail = mailbox + ((seq - 1) % kMailSlots) * 64;
+      }
       const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
       if (edge) tag_chunk<R, TV_EDGE, WIDE>(S, C, c);
       else if (lastStrip && selRow) tag_chunk<R, TV_SEL, WIDE>(S, C, c);
       else tag_chunk<R, TV_FAST, WIDE>(S, C, c);
-      // publish: the chunk ends with the block copy-out store and R trace stores; at vmcnt(R)
-      // the copy-out has completed (vector memory operations complete in order)
-      asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
+      // publish.  LDS mailbox: the block's ds_writes precede the counter's in this wave's LDS
+      // queue.  HBM: the chunk ends with the block store and R trace stores; at vmcnt(R) the
+      // block store has completed (vector memory operations complete in order).
       const int done = rho * nblk + (c < nblk ? c : nblk);
-      if constexpr (WIDE) {
-        if (lane == 0) __hip_atomic_store(gProg + gw, (uint32_t)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (mailOut) {
+        if (lane == 0) __hip_atomic_store(sProg + w, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {
-        if (lane == 0) __hip_atomic_store(sProg + w, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
+        if constexpr (WIDE) {
+          if (lane == 0) __hip_atomic_store(gProg + gw, (uint32_t)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          if (lane == 0) __hip_atomic_store(sProg + w, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
       }
+      if (mailIn && lane == 0)   // release: this chunk's reads of the slot are done
+        __hip_atomic_store(sCons + w, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
 }
