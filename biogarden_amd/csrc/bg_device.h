@@ -101,6 +101,7 @@ struct BgFinishArgs {
   int32_t affine;          // trace carries x/y bits
   int32_t tag;             // tagged linear kernel: 2-bit m_trace codes, boundary rows 4(M+a)+1
   int32_t npairs;
+  int32_t win_bytes;       // LDS trace window (bg_finish_window_bytes)
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

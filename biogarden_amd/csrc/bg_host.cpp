@@ -24,7 +24,8 @@ extern "C" int bg_dp_has_R(int R, int affine, int local, int dna);
 extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide);
 extern "C" int bg_dp_tag_wave_lds_bytes(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
-extern "C" size_t bg_finish_lds_bytes();
+extern "C" size_t bg_finish_lds_bytes(int win_bytes);
+extern "C" int bg_finish_window_bytes(int R, int affine, size_t npairs, int cus);
 extern "C" void* bg_export_kernel_ptr();
 
 #include "bg_tables.inc"
@@ -730,10 +731,11 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.R = h->R;
     F.affine = h->affine;
     F.tag = h->tag;
+    F.win_bytes = bg_finish_window_bytes(h->R, h->affine, np, h->cus);
     F.npairs = (int32_t)np;
     void* args[] = {&F};
     BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(h->R, h->affine, h->mode), dim3(np), dim3(256), args,
-                           bg_finish_lds_bytes(), h->stream2));
+                           bg_finish_lds_bytes(F.win_bytes), h->stream2));
   }
   BG_HIP(hipEventRecord(e[3], h->stream2));
   BG_HIP(hipEventRecord(S.finDone, h->stream2));

@@ -21,6 +21,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "bg_device.h"
 
 #include "bg_dev_util.h"
@@ -406,7 +408,7 @@ __device__ __forceinline__ int unbias(unsigned v) { return (int)(v ^ 0x80000000u
 
 // Trace-window geometry of the finish kernel: a window of 32-step trace blocks of one strip
 // staged in LDS, plus an 8x8 neighbourhood of decoded cells held one per lane.
-constexpr int kWinBytes = 57344;  // 56 KiB window + scalars/scan, under the 64 KiB default
+constexpr int kWinBytesMax = 57344;  // 56 KiB window + scalars/scan, under the 64 KiB default
 constexpr int kCodeMiss = 32, kCodeBorder = 16;
 
 template <int R, bool AFFINE, int MODE>
@@ -415,9 +417,9 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   constexpr int NW = AFFINE ? 4 : 2;
   constexpr int ROWS = BG_WAVE * R;
   constexpr int BLK_DW = R * BG_WAVE * NW;             // dwords per 32-step trace block
-  constexpr int NBW = kWinBytes / (BLK_DW * 4);        // blocks per window
+  const int NBW = F.win_bytes / (BLK_DW * 4);          // blocks per window
   uint32_t* win = reinterpret_cast<uint32_t*>(smem);
-  int* sh = reinterpret_cast<int*>(smem + kWinBytes);  // 64 ints of block-shared scalars
+  int* sh = reinterpret_cast<int*>(smem + F.win_bytes);  // 64 ints of block-shared scalars
   int* scan = sh + 64;                                 // 2 x 256 ints
 
   const BgPair& P = F.pairs[blockIdx.x];
@@ -435,72 +437,77 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   uint8_t* ob = F.out1 + P.out_off;                    // op codes, then aligned seq1 (in place)
   uint8_t* ob2 = F.out2 + P.out_off;
 
-  // ---------------- end cell (aligner.rs:112, 173-176, 247-251, 308-312, 369-389): wave 0
-  if (wid == 0) {
-    int ei = n1, ej = n2, score = 0, colcase = 0;
-    if (mode == BGK_GLOBAL) {
-      score = lastcolM(f, n1);
-    } else if (mode == BGK_LOCAL) {
+  // ---------------- end cell (aligner.rs:112, 173-176, 247-251, 308-312, 369-389): every
+  // thread folds a strided share into 64-bit keys (value, then the index rule), the waves'
+  // keys meet in LDS.  Keys: row/column folds `>= last` and `> first` become max of
+  // (bias(v) << 32 | j) and (bias(v) << 32 | ~i).
+  {
+    u64 ka = 0, kb = 0;
+    const int32_t* rowbest = f.lastcol + (n1 + 1);
+    if (mode == BGK_LOCAL) {
       // first row-major cell with the strict maximum; (0,0) with 0 when nothing is positive
-      u64 key = 0;
-      const int32_t* rowbest = f.lastcol + (n1 + 1);
-      const int32_t* rowpos = rowbest + n1;
-      if (n2 > 0)
-        for (int i = 1 + lane; i <= n1; i += 64) {
+      if (n2 > 0) {
+#pragma unroll 4
+        for (int i = 1 + tid; i <= n1; i += NT) {
           const u64 kk = ((u64)bias(rowbest[i - 1]) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
-          key = kk > key ? kk : key;
+          ka = kk > ka ? kk : ka;
         }
-      key = wave_max_u64(key);
-      const int v = unbias((unsigned)(key >> 32));
-      if (key != 0 && v > 0) {
-        ei = (int)(0xFFFFFFFFu - (unsigned)key);
-        ej = rowpos[ei - 1];
-        score = v;
-      } else {
-        ei = 0; ej = 0; score = 0;
       }
-    } else if (mode == BGK_FITTING) {
-      u64 key = 0;                                   // first i, strict > (:247-249)
-      for (int i = lane; i <= n1; i += 64) {
+    } else if (mode == BGK_FITTING || mode == BGK_SEMIGLOBAL) {
+#pragma unroll 4
+      for (int i = tid; i <= n1; i += NT) {          // last column, first strict max (:247, :376)
         const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
-        key = kk > key ? kk : key;
+        ka = kk > ka ? kk : ka;
       }
-      key = wave_max_u64(key);
-      ei = (int)(0xFFFFFFFFu - (unsigned)key); ej = n2; score = unbias((unsigned)(key >> 32));
-    } else if (mode == BGK_OVERLAP) {
-      u64 key = 0;                                   // last j, >= (:308-310)
-      for (int j = lane; j <= n2; j += 64) {
-        const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
-        key = kk > key ? kk : key;
-      }
-      key = wave_max_u64(key);
-      ei = n1; ej = (int)(unsigned)key; score = unbias((unsigned)(key >> 32));
-    } else {
-      u64 kr = 0, kc = 0;
-      for (int j = lane; j <= n2; j += 64) {         // last row, >= (:369-371)
-        const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
-        kr = kk > kr ? kk : kr;
-      }
-      for (int i = lane; i <= n1; i += 64) {         // last column, > (:376-378)
-        const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
-        kc = kk > kc ? kk : kc;
-      }
-      kr = wave_max_u64(kr);
-      kc = wave_max_u64(kc);
-      const int mr = unbias((unsigned)(kr >> 32)), mc = unbias((unsigned)(kc >> 32));
-      colcase = mc > mr;                             // (:389)
-      if (colcase) { ei = (int)(0xFFFFFFFFu - (unsigned)kc); ej = n2; score = mc; }
-      else { ei = n1; ej = (int)(unsigned)kr; score = mr; }
     }
-    if (lane == 0) { sh[0] = ei; sh[1] = ej; sh[2] = score; sh[3] = colcase; }
+    if (mode == BGK_OVERLAP || mode == BGK_SEMIGLOBAL) {
+#pragma unroll 4
+      for (int j = tid; j <= n2; j += NT) {          // last row, last max (:308, :369)
+        const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
+        kb = kk > kb ? kk : kb;
+      }
+    }
+    ka = wave_max_u64(ka);
+    kb = wave_max_u64(kb);
+    u64* wk = reinterpret_cast<u64*>(scan);          // 2 keys per wave
+    if (lane == 0) { wk[2 * wid] = ka; wk[2 * wid + 1] = kb; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int x = 1; x < NT / 64; ++x) {
+        ka = wk[2 * x] > ka ? wk[2 * x] : ka;
+        kb = wk[2 * x + 1] > kb ? wk[2 * x + 1] : kb;
+      }
+      int ei = n1, ej = n2, score = 0, colcase = 0;
+      if (mode == BGK_GLOBAL) {
+        score = lastcolM(f, n1);
+      } else if (mode == BGK_LOCAL) {
+        const int v = unbias((unsigned)(ka >> 32));
+        if (ka != 0 && v > 0) {
+          ei = (int)(0xFFFFFFFFu - (unsigned)ka);
+          ej = rowbest[n1 + ei - 1];                 // rowpos follows rowbest
+          score = v;
+        } else {
+          ei = 0; ej = 0; score = 0;
+        }
+      } else if (mode == BGK_FITTING) {
+        ei = (int)(0xFFFFFFFFu - (unsigned)ka); ej = n2; score = unbias((unsigned)(ka >> 32));
+      } else if (mode == BGK_OVERLAP) {
+        ei = n1; ej = (int)(unsigned)kb; score = unbias((unsigned)(kb >> 32));
+      } else {
+        const int mr = unbias((unsigned)(kb >> 32)), mc = unbias((unsigned)(ka >> 32));
+        colcase = mc > mr;                           // (:389)
+        if (colcase) { ei = (int)(0xFFFFFFFFu - (unsigned)ka); ej = n2; score = mc; }
+        else { ei = n1; ej = (int)(unsigned)kb; score = mr; }
+      }
+      sh[0] = ei; sh[1] = ej; sh[2] = score; sh[3] = colcase;
+    }
   }
   __syncthreads();
   const int ei = uni(sh[0]), ej = uni(sh[1]), score = uni(sh[2]), colcase = uni(sh[3]);
 
-  // ---------------- semiglobal tail gaps (:389-404): ops written backwards from the slot end
-  // op codes: 0 = (s1, s2), 1 = (s1, '-'), 2 = ('-', s2)
+  // ---------------- semiglobal tail gaps (:389-404): the last ntail columns of the slot; the
+  // walk's op codes (0 = (s1, s2), 1 = (s1, '-'), 2 = ('-', s2)) go backwards in front of them
   const int ntail = (mode == BGK_SEMIGLOBAL) ? (colcase ? n1 - ei : n2 - ej) : 0;
-  for (int x = tid; x < ntail; x += NT) ob[cap - 1 - x] = colcase ? 1 : 2;
 
   // ---------------- traceback walk (aligner.rs:511-592)
   const uint32_t* tr = F.trace + P.trace_off / 4;
@@ -567,6 +574,9 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   for (;;) {
     int reqS = -1, reqB0 = 0, done = 0;
     if (wid == 0) {
+      // the walk is one latency-bound wave: first claim on the issue slots it shares with the
+      // next execute's DP waves (two-stream pipeline)
+      __builtin_amdgcn_s_setprio(3);
       for (;;) {
         int dk = k0 - k, dl = l0 - l;
         if ((unsigned)dk >= 8u || (unsigned)dl >= 8u) { reanchor(k, l); dk = 0; dl = 0; }
@@ -622,6 +632,86 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             state = mvIn == 2 ? 1 : (mvIn == 3 ? 2 : 0);
             continue;
           }
+        } else {
+          // Affine gaps: the same pointer jumping over (cell, state) nodes — 3 per lane, node id
+          // state*64 + lane.  An X (Y) node whose x_trace (y_trace) is 'M' falls back to M
+          // without moving (aligner.rs:566-585), so its next pointer is that cell's M node's.
+          const bool jumpable = !(c & (kCodeMiss | kCodeBorder)) && (MODE != BGK_LOCAL || (c & 3) != 3);
+          if (jumpable) {
+            if ((dk | dl) != 0) { reanchor(k, l); }
+            const int cl = codes;
+            const bool term = (cl & (kCodeMiss | kCodeBorder)) || (MODE == BGK_LOCAL && (cl & 3) == 3);
+            const int mvM = (int)(kLutM >> (4 * (cl & 15)) >> 2) & 3;   // 1 diag, 2 up, 3 left
+            const int mvX = (cl & 4) ? mvM : 2;
+            const int mvY = (cl & 8) ? mvM : 3;
+            int P[3], D[3], OP[3], INFO[3];
+#pragma unroll
+            for (int st = 0; st < 3; ++st) {
+              const int mv = st == 0 ? mvM : (st == 1 ? mvX : mvY);
+              const int nk = (lane >> 3) + (mv != 3), nl = (lane & 7) + (mv != 2);
+              const int ns = mv == 2 ? 1 : (mv == 3 ? 2 : 0);      // state after the move
+              const bool ex = !term && (nk >= 8 || nl >= 8);
+              const int self = st * 64 + lane;
+              P[st] = (term || ex) ? self : ns * 64 + nk * 8 + nl;
+              D[st] = (term || ex) ? 0 : 1;
+              OP[st] = mv - 1;
+              INFO[st] = (ex ? 1 : 0) | (mv << 1) | (ns << 3);
+            }
+            // node value lookup: value of node `node` from the lane holding it
+            auto bperm3 = [&](const int (&v)[3], int node) {
+              const int src = (node & 63) * 4;
+              const int r0 = __builtin_amdgcn_ds_bpermute(src, v[0]);
+              const int r1 = __builtin_amdgcn_ds_bpermute(src, v[1]);
+              const int r2 = __builtin_amdgcn_ds_bpermute(src, v[2]);
+              const int sl = node >> 6;
+              return sl == 0 ? r0 : (sl == 1 ? r1 : r2);
+            };
+            int J[4][3];
+#pragma unroll
+            for (int st = 0; st < 3; ++st) J[0][st] = P[st];
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {                        // p <- p(p), d <- d + d(p)
+              int PK[3];
+#pragma unroll
+              for (int st = 0; st < 3; ++st) PK[st] = P[st] | (D[st] << 8);
+#pragma unroll
+              for (int st = 0; st < 3; ++st) {
+                const int qv = bperm3(PK, P[st]);
+                P[st] = qv & 255;
+                D[st] += qv >> 8;
+              }
+              if (rr < 3) {
+#pragma unroll
+                for (int st = 0; st < 3; ++st) J[rr + 1][st] = P[st];
+              }
+            }
+            const int entry = state * 64;                           // (anchor cell, state)
+            int x = entry;
+#pragma unroll
+            for (int bb = 0; bb < 4; ++bb) {
+              const int y = bperm3(J[bb], x);
+              x = ((lane >> bb) & 1) ? y : x;
+            }
+            const int opx = bperm3(OP, x);
+            const int Pn = rdlane(state == 0 ? P[0] : (state == 1 ? P[1] : P[2]), 0);
+            const int Dn = rdlane(state == 0 ? D[0] : (state == 1 ? D[1] : D[2]), 0);
+            const int sP = Pn >> 6, lP = Pn & 63;
+            const int infoP = rdlane(sP == 0 ? INFO[0] : (sP == 1 ? INFO[1] : INFO[2]), lP);
+            const int exP = infoP & 1, mvP = (infoP >> 1) & 3, nsP = infoP >> 3;
+            const int nops = Dn + exP;
+            if (lane < nops) ob[cap - 1 - (ntail + ncore + lane)] = (uint8_t)opx;
+            ncore += nops;
+            k -= lP >> 3;
+            l -= lP & 7;
+            if (exP) {
+              k -= (mvP != 3);
+              l -= (mvP != 2);
+              state = nsP;
+            } else {
+              state = sP;
+            }
+            continue;
+          }
         }
         if (c & kCodeMiss) {
           const int vr = k - 1;
@@ -649,6 +739,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           ++ncore;
         }
       }
+      __builtin_amdgcn_s_setprio(0);
       if (lane == 0) { sh[4] = reqS; sh[5] = reqB0; sh[6] = done; }
     }
     __syncthreads();
@@ -689,17 +780,27 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   ncore = sh[10];
   int npre = 0;
   if (status == 0 && mode == BGK_SEMIGLOBAL) npre = colcase ? kstop : lstop;
-  for (int x = tid; x < npre; x += NT) ob[cap - 1 - (ntail + ncore + x)] = colcase ? 1 : 2;
   const int L = ntail + ncore + npre;
-  __syncthreads();
-
-  // ---------------- expand ops into the two aligned strings (parallel scan over columns)
-  int i0 = kstop, j0 = lstop;                          // first residues the columns consume
-  if (mode == BGK_SEMIGLOBAL && status == 0) { if (colcase) i0 = 0; else j0 = 0; }
   const int base = cap - L;
-  const int seg = (L + NT - 1) / NT;
-  const int lo = base + tid * seg < cap ? base + tid * seg : cap;
-  const int hi = lo + seg < cap ? lo + seg : cap;
+
+  // ---------------- semiglobal prefix (:416-428) and tail columns: one residue run against gaps
+  // each (prefix: s1[0, kstop) or s2[0, lstop); tail: s1[ei, n1) or s2[ej, n2))
+  for (int x = tid; x < npre; x += NT) {
+    ob[base + x] = colcase ? f.s1[x] : (uint8_t)'-';
+    ob2[base + x] = colcase ? (uint8_t)'-' : f.s2[x];
+  }
+  for (int x = tid; x < ntail; x += NT) {
+    ob[cap - ntail + x] = colcase ? f.s1[ei + x] : (uint8_t)'-';
+    ob2[cap - ntail + x] = colcase ? (uint8_t)'-' : f.s2[ej + x];
+  }
+
+  // ---------------- expand the walk's op codes into both strings (parallel scan over columns)
+  const int i0 = kstop, j0 = lstop;                    // first residues the core consumes
+  const int cbase = base + npre;
+  const int seg = (ncore + NT - 1) / NT;
+  const int cend = cbase + ncore;
+  const int lo = cbase + tid * seg < cend ? cbase + tid * seg : cend;
+  const int hi = lo + seg < cend ? lo + seg : cend;
   int c1 = 0, c2 = 0;
   for (int x = lo; x < hi; ++x) { const int op = ob[x]; c1 += op != 2; c2 += op != 1; }
   scan[tid] = c1;
@@ -839,4 +940,12 @@ extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode) {
 extern "C" int bg_dp_has_R(int R, int affine, int local, int dna) {
   return bg_dp_kernel_ptr(R, affine, local, dna) != nullptr;
 }
-extern "C" size_t bg_finish_lds_bytes() { return kWinBytes + 64 * 4 + 2 * 256 * 4; }
+// Trace window of the finish kernel: the full 56 KiB (2 workgroups per CU) for few long pairs;
+// for batches of many pairs a smaller window (>= 8 blocks) lets more pairs walk per CU.
+extern "C" int bg_finish_window_bytes(int R, int affine, size_t npairs, int cus) {
+  const int blk = R * BG_WAVE * (affine ? 4 : 2) * 4;
+  if (npairs <= (size_t)cus * 2) return kWinBytesMax / blk * blk;
+  int w = std::max(8 * blk, 20480);
+  return std::min(w, kWinBytesMax) / blk * blk;
+}
+extern "C" size_t bg_finish_lds_bytes(int win_bytes) { return (size_t)win_bytes + 64 * 4 + 2 * 256 * 4; }
