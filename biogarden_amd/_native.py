@@ -48,6 +48,7 @@ class BgStats(ctypes.Structure):
                 ("dna", ctypes.c_int32),
                 ("local", ctypes.c_int32), ("npairs", ctypes.c_int32),
                 ("wide", ctypes.c_int32), ("workgroups", ctypes.c_int32),
+                ("checkpoint", ctypes.c_int32),
                 ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float)]
 
 
@@ -135,8 +136,11 @@ class Handle:
     def set_tuning(self, R=0, waves=0):
         check(lib().bg_set_tuning(self._p, R, waves))
 
-    def set_kernel_options(self, allow_tagged=True):
-        check(lib().bg_set_kernel_options(self._p, 1 if allow_tagged else 0))
+    def set_kernel_options(self, allow_tagged=True, checkpoint=True):
+        """allow_tagged: tagged linear kernel (else mask trace); checkpoint: score-only DP with
+        the traceback recomputing the chunks it crosses (else the full trace is written)."""
+        check(lib().bg_set_kernel_options(self._p, (1 if allow_tagged else 0) |
+                                          (2 if (allow_tagged and checkpoint) else 0)))
 
     def set_pipeline(self, depth):
         check(lib().bg_set_pipeline(self._p, depth))

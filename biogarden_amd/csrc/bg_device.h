@@ -99,9 +99,14 @@ struct BgFinishArgs {
   int32_t mode;
   int32_t R;               // rows per lane of the DP kernel that produced the trace
   int32_t affine;          // trace carries x/y bits
-  int32_t tag;             // tagged linear kernel: 2-bit m_trace codes, boundary rows 4(M+a)+1
+  int32_t tag;             // 1: tagged linear kernel (2-bit m_trace codes, boundary rows X forms);
+                           // 2: checkpoint traceback (untagged M' boundary rows, no trace)
   int32_t npairs;
   int32_t win_bytes;       // LDS trace window (bg_finish_window_bytes)
+  // checkpoint traceback (tag == 2): trace = checkpoint arena; recomputation inputs
+  const uint8_t* codes1;
+  const uint8_t* codes2;
+  const int32_t* profile;
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

@@ -21,7 +21,9 @@
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
 extern "C" int bg_dp_has_R(int R, int affine, int local, int dna);
-extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide);
+extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt);
+extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode);
+extern "C" size_t bg_finish_ck_lds_bytes(int R, int* win_bytes);
 extern "C" int bg_dp_tag_wave_lds_bytes(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes(int win_bytes);
@@ -95,6 +97,8 @@ struct bg_aligner {
   std::vector<size_t> order_;        // plan slot -> caller index
   int R = 8, W = 1, affine = 0, local = 0, dna = 1, kdim = 0, tag = 0;
   int allowTag = 1;
+  int allowCkpt = 1;
+  int ckpt = 0;                    // tagged path: score-only DP + checkpoint traceback
   size_t lds = 0;
   int progOff = 256;
   int codesOff = 320;
@@ -218,7 +222,8 @@ extern "C" int bg_set_tuning(bg_aligner* h, int R, int waves) {
 
 extern "C" int bg_set_kernel_options(bg_aligner* h, int allow_tagged) {
   if (!h) return BG_E_ARG;
-  h->allowTag = allow_tagged ? 1 : 0;
+  h->allowTag = (allow_tagged & 1) ? 1 : 0;
+  h->allowCkpt = (allow_tagged & 2) ? 1 : 0;
   h->prepared = false;
   h->executed = false;
   return BG_OK;
@@ -321,11 +326,12 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   std::vector<int> start, end, diff;
   for (int Rc : cand) {
     if (h->tuneR && Rc != h->tuneR) continue;
-    if (!(h->tag ? bg_dp_kernel_tag_ptr(Rc, 0) != nullptr : bg_dp_has_R(Rc, h->affine, h->local, h->dna))) continue;
-    const void* fn = h->tag ? bg_dp_kernel_tag_ptr(Rc, 0) : bg_dp_kernel_ptr(Rc, h->affine, h->local, h->dna);
+    if (!(h->tag ? bg_dp_kernel_tag_ptr(Rc, 0, h->ckpt) != nullptr : bg_dp_has_R(Rc, h->affine, h->local, h->dna))) continue;
+    const void* fn = h->tag ? bg_dp_kernel_tag_ptr(Rc, 0, h->ckpt) : bg_dp_kernel_ptr(Rc, h->affine, h->local, h->dna);
     const int vg = vgprs_of(fn);
-    const int fin = h->depth > 1 ? vgprs_of(bg_finish_kernel_ptr(Rc, h->affine, h->mode)) : 0;
-    const int opsPerStep = h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12);
+    const void* ffn = h->ckpt ? bg_finish_ck_kernel_ptr(Rc, h->mode) : bg_finish_kernel_ptr(Rc, h->affine, h->mode);
+    const int fin = h->depth > 1 ? vgprs_of(ffn) : 0;
+    const int opsPerStep = h->ckpt ? 2 * Rc + 2 : (h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12));
     const int S = maxn1 ? (int)((maxn1 + 64 * Rc - 1) / (64 * Rc)) : 1;
     const int wmax = (h->affine || h->local) ? 8 : 16;
     for (int Wc = 1; Wc <= wmax; ++Wc) {
@@ -478,6 +484,7 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
         if (v - 3 < -128 || v - 2 > 127) tagOK = false;
       }
   h->tag = tagOK ? 1 : 0;
+  h->ckpt = (h->tag && h->allowCkpt) ? 1 : 0;
 
   // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair, or a group
   // of workgroups per pair in the tagged kernel's WIDE mode)
@@ -551,7 +558,10 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     P.pad = P.nstrips * 64 * R - P.n1;
     P.nc = (int32_t)(n2[p] / 64 + 2);
     P.trace_off = tro;
-    tro += round_up((uint64_t)P.nstrips * P.nc * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE * 4, 256);
+    if (h->ckpt)   // checkpoints: R + 1 ints per lane per chunk
+      tro += round_up((uint64_t)P.nstrips * P.nc * (R + 1) * BG_WAVE * 4, 256);
+    else
+      tro += round_up((uint64_t)P.nstrips * P.nc * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE * 4, 256);
     P.bnd_off = bo;
     bo += (uint64_t)P.nstrips * P.nc * BG_CHUNK;
     P.aux_off = ao;
@@ -622,6 +632,11 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
         }
         prof[64 + dense[q]] = (int32_t)px;
         prof[128 + dense[q]] = (int32_t)py;
+        uint32_t pz = 0;                       // score-only pass: S - 2a, untagged
+        for (int c = 0; c < 32; ++c)
+          if (dense[c] >= 0)
+            pz |= (uint32_t)(uint8_t)(int8_t)(sc->table[q * 32 + c] - 2 * a) << (8 * dense[c]);
+        prof[192 + dense[q]] = (int32_t)pz;
       }
     }
   } else {
@@ -679,7 +694,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[0], h->stream));
   if (np) {
-    void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide) : bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
+    void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
     A.pairs = h->pairs.as<BgPair>();
@@ -730,12 +745,24 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.mode = h->mode;
     F.R = h->R;
     F.affine = h->affine;
-    F.tag = h->tag;
-    F.win_bytes = bg_finish_window_bytes(h->R, h->affine, np, h->cus);
+    F.tag = h->ckpt ? 2 : h->tag;
     F.npairs = (int32_t)np;
+    F.codes1 = h->codes1.as<uint8_t>();
+    F.codes2 = h->codes2.as<uint8_t>();
+    F.profile = h->prof.as<int32_t>();
     void* args[] = {&F};
-    BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(h->R, h->affine, h->mode), dim3(np), dim3(256), args,
-                           bg_finish_lds_bytes(F.win_bytes), h->stream2));
+    if (h->ckpt) {
+      int win = 0;
+      const size_t lds = bg_finish_ck_lds_bytes(h->R, &win);
+      F.win_bytes = win;
+      void* ffn = bg_finish_ck_kernel_ptr(h->R, h->mode);
+      if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(256), args, lds, h->stream2));
+    } else {
+      F.win_bytes = bg_finish_window_bytes(h->R, h->affine, np, h->cus);
+      BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(h->R, h->affine, h->mode), dim3(np), dim3(256), args,
+                             bg_finish_lds_bytes(F.win_bytes), h->stream2));
+    }
   }
   BG_HIP(hipEventRecord(e[3], h->stream2));
   BG_HIP(hipEventRecord(S.finDone, h->stream2));
@@ -848,6 +875,7 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->wide = h->wide;
   o->workgroups = h->gridWgs;
   o->tagged = h->tag;
+  o->checkpoint = h->ckpt;
   o->dna = h->dna;
   o->local = h->local;
   o->npairs = (int32_t)h->npairs;

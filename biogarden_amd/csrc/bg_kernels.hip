@@ -26,6 +26,7 @@
 #include "bg_device.h"
 
 #include "bg_dev_util.h"
+#include "bg_tag_common.h"
 
 using namespace bgk;
 
@@ -382,6 +383,8 @@ __device__ __forceinline__ int lastrowM(const Fin& f, int j) {
   if (j == 0) return col0_M(f.mode, f.n1, f.a, f.b);
   const int v = f.lastrowMa[j];
   // the tagged kernel stores X forms 4*(M(n1,j) - a*(n1+j)) + 2
+  // checkpoint mode (tag 2) stores M'(n1,j) = M(n1,j) - a*(n1+j) itself
+  if (f.F->tag == 2) return wadd(v, wmul(f.a, f.n1 + j));
   return f.F->tag ? wadd(v >> 2, wmul(f.a, f.n1 + j)) : wadd(v, -f.a);
 }
 __device__ __forceinline__ int lastcolM(const Fin& f, int i) {
@@ -411,7 +414,78 @@ __device__ __forceinline__ int unbias(unsigned v) { return (int)(v ^ 0x80000000u
 constexpr int kWinBytesMax = 57344;  // 56 KiB window + scalars/scan, under the 64 KiB default
 constexpr int kCodeMiss = 32, kCodeBorder = 16;
 
-template <int R, bool AFFINE, int MODE>
+// ------------------------------------------------------------------ checkpoint traceback
+// One wave recomputes chunk c of strip s of a pair from the forward pass's checkpoint with the
+// tagged step (tag_chunk<KIND_RECOMP>, the same arithmetic as the tagged forward kernel) and
+// leaves the chunk's 2-bit trace in an LDS slot laid out like the HBM trace of two 32-step
+// blocks: [h][row k][lane] x uint2.
+constexpr int kCkSlots = 8;
+template <int R>
+__host__ __device__ constexpr int ck_slot_dw() { return 2 * R * BG_WAVE * 2; }
+template <int R>
+__host__ __device__ constexpr int ck_wave_ints() { return 64 + 4 * 64 * ProfW<R>::v + 96; }
+
+template <int R>
+__device__ void recompute_chunk(const BgFinishArgs& F, const BgPair& P, int s, int c,
+                                uint32_t* slot, int* area, int lane) {
+  constexpr int RW = ProfW<R>::v;
+  const int n1 = P.n1, n2 = P.n2, NC = P.nc;
+  const int a = F.open, b = F.ext, mode = F.mode;
+  int* bIn = area;
+  int* profTab = area + 64;
+  uint16_t* stage = reinterpret_cast<uint16_t*>(profTab + 4 * 64 * RW);
+  TagCtx C;
+  TagStrip<R> S;
+  C.a = a; C.b = b; C.mode = mode; C.n1 = n1; C.n2 = n2; C.lane = lane;
+  C.rowbase = s * BG_WAVE * R + lane * R;
+  C.orow = R - 1;
+  C.lastcol = nullptr; C.ring = nullptr; C.oLane = nullptr; C.mail = nullptr; C.bndOut = nullptr;
+  const uint8_t* c1 = F.codes1 + P.off1;
+  const uint8_t* g2 = F.codes2 + P.off2;
+  int pk[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = C.rowbase + k + 1;
+    const int q = (i <= n1) ? c1[i - 1] : 0;
+    pk[k] = F.profile[(k == 0 ? 64 : 128) + (q >> 3)];
+  }
+#pragma unroll
+  for (int cd = 0; cd < 4; ++cd)
+#pragma unroll
+    for (int wd = 0; wd < RW; ++wd) {
+      unsigned v = 0;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+        if (wd * 4 + bb < R) v |= (((unsigned)pk[wd * 4 + bb] >> (8 * cd)) & 0xffu) << (8 * bb);
+      profTab[(cd * 64 + lane) * RW + wd] = (int)v;
+    }
+#pragma unroll
+  for (int q = 0; q < 3; ++q) {
+    const int x = c * BG_CHUNK - 64 + lane + 64 * q;
+    const int v = g2[x < 0 ? 0 : (x >= n2 ? n2 - 1 : x)];
+    stage[lane + 64 * q] = (uint16_t)(((unsigned)x < (unsigned)n2) ? v * (32 * RW) : 0);
+  }
+  const int jb = c * BG_CHUNK + lane;
+  if (s == 0) {
+    bIn[lane] = 4 * wadd(row0_M(mode, jb, a, b), -wmul(a, jb)) + 2;
+  } else {
+    bIn[lane] = 4 * F.bndM[P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb] + 2;
+  }
+  const int32_t* ck = reinterpret_cast<const int32_t*>(F.trace + P.trace_off / 4) +
+                      ((size_t)(s * NC + c) * (R + 1)) * BG_WAVE + lane;
+#pragma unroll
+  for (int k = 0; k < R; ++k) { S.Y[k] = 4 * ck[k * BG_WAVE] + 3; S.tA[k] = 0; S.tB[k] = 0; }
+  S.topPrev = 4 * ck[R * BG_WAVE] + 2;
+  S.Xlast = S.Y[R - 1] - 1;
+  C.bIn = bIn;
+  C.profLane = reinterpret_cast<const uint8_t*>(profTab + lane * RW);
+  C.codeLane = stage + 63 - lane;
+  C.trace = slot - (size_t)(2 * c) * (R * 2 * BG_WAVE);    // tag_chunk adds ((t0 >> 5) + h) blocks
+  if (c == 0) tag_chunk<R, TV_EDGE, false, KIND_RECOMP>(S, C, c);
+  else tag_chunk<R, TV_FAST, false, KIND_RECOMP>(S, C, c);
+}
+
+template <int R, bool AFFINE, int MODE, bool CK = false>
 __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int NW = AFFINE ? 4 : 2;
@@ -421,6 +495,9 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   uint32_t* win = reinterpret_cast<uint32_t*>(smem);
   int* sh = reinterpret_cast<int*>(smem + F.win_bytes);  // 64 ints of block-shared scalars
   int* scan = sh + 64;                                 // 2 x 256 ints
+  // checkpoint mode: the window is kCkSlots recomputed chunks; sh[16+z] / sh[24+z] = strip /
+  // chunk held by slot z (-1: empty); per-wave recompute areas follow the scan
+  int* ckArea = scan + 2 * 256;
 
   const BgPair& P = F.pairs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6), NT = blockDim.x;
@@ -539,6 +616,10 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     for (int c = 0; c < 16; ++c) v |= (u64)((c & 8) ? 0 : ((3u << 2) | 2)) << (4 * c);
     return v;
   }();
+  int ckS[kCkSlots], ckC[kCkSlots];                  // checkpoint mode: resident chunks
+  int ckNext = 0;                                    // next slot to fill (FIFO)
+#pragma unroll
+  for (int z = 0; z < kCkSlots; ++z) { ckS[z] = -1; ckC[z] = -1; }
   // decodes the 8x8 neighbourhood anchored at (k, l): lane (dk, dl) holds cell (k - dk, l - dl)
   auto reanchor = [&](int ka, int la) {
     k0 = ka; l0 = la;
@@ -549,7 +630,22 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       const int vr = kk - 1;
       const int sidx = vr / ROWS, rem = vr - sidx * ROWS, r = rem / R, q = rem - r * R;
       const int t = ll + r, bl = t >> 5;
-      if (sidx != curS || bl < curB0 || bl >= curB0 + curNb) {
+      if constexpr (CK) {
+        const int cc = t >> 6;
+        int z = -1;
+#pragma unroll
+        for (int zz = 0; zz < kCkSlots; ++zz)
+          if (ckS[zz] == sidx && ckC[zz] == cc) z = zz;
+        if (z < 0) {
+          codes = kCodeMiss;
+        } else {
+          const uint32_t* wp = win + (size_t)z * ck_slot_dw<R>() + (((bl & 1) * R + q) * BG_WAVE + r) * 2;
+          const uint2 v = *reinterpret_cast<const uint2*>(wp);
+          const int u = t & 31;
+          const int tg = (int)((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3;
+          codes = ((0x2100 >> (4 * tg)) & 3) | 12;
+        }
+      } else if (sidx != curS || bl < curB0 || bl >= curB0 + curNb) {
         codes = kCodeMiss;
       } else {
         const uint32_t* wp = win + (((bl - curB0) * R + q) * BG_WAVE + r) * NW;
@@ -717,7 +813,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           const int vr = k - 1;
           reqS = vr / ROWS;
           const int bl = (l + (vr - reqS * ROWS) / R) >> 5;
-          reqB0 = bl - NBW + 1 > 0 ? bl - NBW + 1 : 0;
+          reqB0 = CK ? (bl >> 1) : (bl - NBW + 1 > 0 ? bl - NBW + 1 : 0);
           break;
         }
         const bool interior = !(c & kCodeBorder);
@@ -747,7 +843,31 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     if (done) break;
     reqS = uni(sh[4]);
     reqB0 = uni(sh[5]);
-    {
+    if constexpr (CK) {
+      // recompute the requested chunk and up to three chunks to its left (the walk heads up and
+      // left), one per wave, into the oldest slots
+      int list[4], nl = 0;
+      for (int d = 0; d < 4; ++d) {
+        const int cc = reqB0 - d;
+        if (cc < 0) break;
+        bool res = false;
+#pragma unroll
+        for (int z = 0; z < kCkSlots; ++z) res |= (ckS[z] == reqS && ckC[z] == cc);
+        if (!res || d == 0) list[nl++] = cc;
+      }
+      const int myz = (ckNext + wid) % kCkSlots;
+      if (wid < nl)
+        recompute_chunk<R>(F, P, reqS, list[wid], win + (size_t)myz * ck_slot_dw<R>(),
+                           ckArea + wid * ck_wave_ints<R>(), lane);
+      for (int x = 0; x < nl; ++x) {
+        const int z = (ckNext + x) % kCkSlots;
+#pragma unroll
+        for (int zz = 0; zz < kCkSlots; ++zz)
+          if (zz == z) { ckS[zz] = reqS; ckC[zz] = list[x]; }
+      }
+      ckNext = (ckNext + nl) % kCkSlots;
+      k0 = -1000000;
+    } else {
       const int nb = (stripBlocks - reqB0) < NBW ? (stripBlocks - reqB0) : NBW;
       const uint4* src = reinterpret_cast<const uint4*>(tr + (size_t)reqS * stripDw + (size_t)reqB0 * BLK_DW);
       uint4* dst = reinterpret_cast<uint4*>(win);
@@ -914,6 +1034,43 @@ extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna) {
     return local ? (void*)&bg_dp_kernel<10, false, true, true> : (void*)&bg_dp_kernel<10, false, false, true>;
   }
   return nullptr;
+}
+
+template <int R>
+static void* finish_ck_ptr(int mode) {
+  switch (mode) {
+    case BGK_GLOBAL: return (void*)&bg_finish_kernel<R, false, BGK_GLOBAL, true>;
+    case BGK_FITTING: return (void*)&bg_finish_kernel<R, false, BGK_FITTING, true>;
+    case BGK_OVERLAP: return (void*)&bg_finish_kernel<R, false, BGK_OVERLAP, true>;
+    case BGK_SEMIGLOBAL: return (void*)&bg_finish_kernel<R, false, BGK_SEMIGLOBAL, true>;
+    default: return nullptr;
+  }
+}
+// checkpoint traceback (linear gaps, non-local): the finish kernel over recomputed chunks
+extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode) {
+  switch (R) {
+    case 2: return finish_ck_ptr<2>(mode);
+    case 3: return finish_ck_ptr<3>(mode);
+    case 4: return finish_ck_ptr<4>(mode);
+    case 5: return finish_ck_ptr<5>(mode);
+    case 8: return finish_ck_ptr<8>(mode);
+    case 10: return finish_ck_ptr<10>(mode);
+    default: return nullptr;
+  }
+}
+// LDS of the checkpoint finish kernel: chunk slots, scalars + scan, 4 recompute areas
+extern "C" size_t bg_finish_ck_lds_bytes(int R, int* win_bytes) {
+  int slot = 0, area = 0;
+  switch (R) {
+    case 2: slot = ck_slot_dw<2>(); area = ck_wave_ints<2>(); break;
+    case 3: slot = ck_slot_dw<3>(); area = ck_wave_ints<3>(); break;
+    case 4: slot = ck_slot_dw<4>(); area = ck_wave_ints<4>(); break;
+    case 5: slot = ck_slot_dw<5>(); area = ck_wave_ints<5>(); break;
+    case 8: slot = ck_slot_dw<8>(); area = ck_wave_ints<8>(); break;
+    default: slot = ck_slot_dw<10>(); area = ck_wave_ints<10>(); break;
+  }
+  *win_bytes = kCkSlots * slot * 4;
+  return (size_t)*win_bytes + 64 * 4 + 2 * 256 * 4 + 4 * (size_t)area * 4;
 }
 
 template <int R, bool AF>

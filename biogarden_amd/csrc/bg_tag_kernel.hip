@@ -33,164 +33,9 @@
 #include <stdint.h>
 
 #include "bg_dev_util.h"
+#include "bg_tag_common.h"
 
 using namespace bgk;
-
-namespace {
-
-template <int R>
-struct TagStrip {
-  int Y[R];           // Y form of (i_k, j-1): 4*M'(i_k, j-1) + 3
-  unsigned tA[R];     // trace codes of steps 0-15 of the current 32-step block (2 bits each)
-  unsigned tB[R];     // steps 16-31
-  int topPrev;        // X form of (row above, j-1) for the lane's first row
-  int Xlast;          // X form of (lane's last row, j): handed down to lane r+1 by DPP
-};
-
-struct TagCtx {
-  int a, b, mode, n1, n2, rowbase, orow, lane;
-  uint32_t* trace;          // this strip's trace
-  int32_t* bndOut;          // this strip's boundary row (X forms), 64-column blocks
-  int32_t* lastcol;         // M(i, n2)
-  const int* bIn;           // LDS: staged boundary block of the strip above (64 X forms)
-  int* ring;                // LDS: this wave's 256-slot output ring
-  int* oLane;               // LDS: this lane's ring write base (slot = u + 64 - lane [+128])
-  const uint16_t* codeLane; // LDS: this chunk's scaled codes, + u = column t0 + u - lane
-  int* mail;                // LDS mailbox slot for the block finished in this chunk (consumer
-                            // in this workgroup), or nullptr: the block goes to HBM
-  const uint8_t* profLane;  // LDS: this lane's profile entries (+ scaled code = entry address)
-};
-
-// profile dwords per lane and code: R int8 bytes, padded to an aligned ds_read width
-template <int R>
-struct ProfW { static constexpr int v = R <= 4 ? 1 : (R <= 8 ? 2 : 4); };
-
-template <int RW>
-struct ProfV { int w[RW]; };
-
-template <int RW>
-__device__ __forceinline__ ProfV<RW> load_prof(const uint8_t* p) {
-  ProfV<RW> r;
-  if constexpr (RW == 1) {
-    r.w[0] = *reinterpret_cast<const int*>(p);
-  } else if constexpr (RW == 2) {
-    const int2 v = *reinterpret_cast<const int2*>(p);
-    r.w[0] = v.x; r.w[1] = v.y;
-  } else {
-    const int4 v = *reinterpret_cast<const int4*>(p);
-    r.w[0] = v.x; r.w[1] = v.y; r.w[2] = v.z; r.w[3] = v.w;
-  }
-  return r;
-}
-
-// x + sign_extend(byte `sel` of w): written as a constant-offset v_bfe_i32 + v_add, which the
-// SDWA peephole folds into one v_add_u32_sdwa ... sext src1_sel:BYTE_sel
-__device__ __forceinline__ int add_sbyte(int x, int w, int sel) {
-  return x + __builtin_amdgcn_sbfe(w, 8 * sel, 8);
-}
-
-enum { TV_FAST = 0, TV_SEL = 1, TV_EDGE = 2 };
-
-// Y form of column 0, row i: 4*(M(i,0) - a*i) + 3 (aligner.rs:98-104 borders)
-__device__ __forceinline__ int col0_Y(int mode, int i, int a, int b) {
-  return 4 * wadd(col0_M(mode, i, a, b), -wmul(a, i)) + 3;
-}
-
-template <int R, int VAR, bool WIDE>
-__device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c) {
-  const int a = C.a;
-  const int t0 = c * BG_CHUNK;
-  const int lane = C.lane;
-  constexpr int RW = ProfW<R>::v;
-  // operand pipeline: the code of step u+2 and the profile entry of step u+1 are in flight
-  // while step u computes
-  int nTop = C.bIn[0];
-  ProfV<RW> nP = load_prof<RW>(C.profLane + C.codeLane[0]);
-  int nCode = C.codeLane[1];
-  const uint16_t* cl = C.codeLane + 2;   // advanced by 32 per half: immediate offsets inside
-  const int* bi = C.bIn + 1;
-#pragma unroll 1
-  for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h, cl += BG_TRACE_BLK, bi += BG_TRACE_BLK) {
-#pragma unroll
-    for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
-      const int u = h * BG_TRACE_BLK + uu;
-      const int t = t0 + u;
-      const int topIn = nTop;
-      const ProfV<RW> P = nP;
-      nP = load_prof<RW>(C.profLane + nCode);
-      nCode = cl[uu];
-      nTop = bi[uu];
-      const int topX = dpp_shr1(topIn, S.Xlast);             // X form of (row above, j)
-      int dIn = S.topPrev;                                    // X form of (row above, j-1)
-      int xo = topX;
-#pragma unroll
-      for (int k = 0; k < R; ++k) {
-        const int yo = S.Y[k];
-        const int d = add_sbyte(dIn, P.w[k >> 2], k & 3);      // 4*(M'(i-1,j-1) + S - 2a), tag 0
-        const int best = imax(imax(d, xo), yo);
-        // append the 2-bit code; the empty asm pins each update to its step (otherwise LLVM
-        // sinks all 16 alignbits to the flush and keeps every step's `best` live)
-        if (uu < 16) { S.tA[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tA[k], 2); asm volatile("" : "+v"(S.tA[k])); }
-        else { S.tB[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tB[k], 2); asm volatile("" : "+v"(S.tB[k])); }
-        const int yn = best | 3;                              // Y form for column j+1
-        dIn = yo;
-        xo = yn - 1;                                          // X form for row i+1
-        S.Y[k] = yn;
-      }
-      S.topPrev = topX;
-      S.Xlast = xo;
-      if constexpr (VAR == TV_EDGE) {
-        if (c == 0) {                                         // column 0 (aligner.rs:98-104)
-          const bool rst = (t == lane);
-#pragma unroll
-          for (int k = 0; k < R; ++k) {
-            const int i = C.rowbase + k + 1;
-            S.Y[k] = rst ? col0_Y(C.mode, i, a, C.b) : S.Y[k];
-          }
-          S.Xlast = rst ? S.Y[R - 1] - 1 : S.Xlast;
-        }
-        if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {    // column n2: M(i, n2)
-          if (lane == t - C.n2) {
-#pragma unroll
-            for (int k = 0; k < R; ++k) {
-              const int i = C.rowbase + k + 1;
-              if (i <= C.n1) C.lastcol[i] = wadd(S.Y[k] >> 2, wmul(a, i + C.n2));
-            }
-          }
-        }
-      }
-      int out = S.Xlast;
-      if constexpr (VAR != TV_FAST) {
-#pragma unroll
-        for (int k = 0; k < R - 1; ++k) out = (C.orow == k) ? S.Y[k] - 1 : out;
-      }
-      C.oLane[u] = out;
-      // one step per scheduling region: hoisting later steps' profile lookups spills
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (h == 1 && c >= 1) {
-      // block c-1 (ring slots 0-63) is final: copy it out, slide the ring by one block
-      const int v = C.ring[lane];
-      const int nx = C.ring[64 + lane];
-      if (C.mail)           // the next strip runs on a wave of this workgroup
-        C.mail[lane] = v;
-      else if constexpr (WIDE)   // read by workgroups on other XCDs: agent-coherent store
-        __hip_atomic_store(C.bndOut + (c - 1) * BG_CHUNK + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else
-        C.bndOut[(c - 1) * BG_CHUNK + lane] = v;
-      C.ring[lane] = nx;
-    } else if (h == 1) {
-      C.ring[lane] = C.ring[64 + lane];
-    }
-    // trace flush every 32 steps: block b, row k, lane r -> dwords [((b*R + k)*64 + r)*2, +2)
-    uint32_t* tb = C.trace + (size_t)((t0 >> 5) + h) * (R * 2 * BG_WAVE) + lane * 2;
-#pragma unroll
-    for (int k = 0; k < R; ++k)
-      *reinterpret_cast<uint2*>(tb + k * 2 * BG_WAVE) = make_uint2(S.tA[k], S.tB[k]);
-  }
-}
-
-}  // namespace
 
 // LDS layout (bytes from the dynamic base; the host sizes it in bg_host.cpp):
 //   16 produced + 16 consumed counters (128 B, @prog_off) | the pair's scaled code row when it
@@ -217,7 +62,10 @@ __host__ __device__ constexpr int tag_wave_ints() {
   return kTagWaveInts + 4 * 64 * ProfW<R>::v + kTagStageU16 / 2 + kMailSlots * 64;
 }
 
-template <int R, bool WIDE>
+// CKPT: the score-only forward pass of the checkpoint traceback (score_chunk, untagged M'
+// values); at every chunk start each lane stores its R values and topPrev to the checkpoint
+// arena: ckpt[((s * NC + c) * (R + 1) + k) * 64 + lane] (k = R: topPrev).
+template <int R, bool WIDE, bool CKPT>
 __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int RW = ProfW<R>::v;
@@ -322,8 +170,13 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     for (int k = 0; k < R; ++k) {
       const int i = C.rowbase + k + 1;
       const int q = (i <= n1) ? qk[k] : 0;
-      pk[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];   // 4 codes x int8
-      S.Y[k] = col0_Y(mode, i, a, b);
+      if constexpr (CKPT) {
+        pk[k] = A.profile[192 + (q >> 3)];                // 4 codes x int8 S - 2a
+        S.Y[k] = wadd(col0_M(mode, i, a, b), -wmul(a, i));
+      } else {
+        pk[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];   // 4 codes x int8
+        S.Y[k] = col0_Y(mode, i, a, b);
+      }
       S.tA[k] = 0; S.tB[k] = 0;
     }
     // this lane's profile entries: for code cd, dword wd holds rows 4wd..4wd+3
@@ -337,7 +190,10 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
           if (wd * 4 + bb < R) v |= (((unsigned)pk[wd * 4 + bb] >> (8 * cd)) & 0xffu) << (8 * bb);
         profTab[(cd * 64 + lane) * RW + wd] = (int)v;
       }
-    S.topPrev = 0; S.Xlast = 2;
+    S.topPrev = 0; S.Xlast = CKPT ? 0 : 2;
+    int32_t* ckBase = CKPT ? reinterpret_cast<int32_t*>(A.trace + P.trace_off / 4) +
+                                 (size_t)s * NC * (R + 1) * BG_WAVE + lane
+                           : nullptr;
     int cv[3] = {0, 0, 0};
     if (!rowInLds) fetch_codes(0, cv);
     for (int c = 0; c < NC; ++c) {
@@ -352,7 +208,8 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       const int seq = rho * NC + c;                              // block sequence number
       const int jb = c * BG_CHUNK + lane;
       if (s == 0) {
-        waveLds[lane] = 4 * wadd(row0_M(mode, jb, a, b), -wmul(a, jb)) + 2;   // X form of row 0
+        const int m0 = wadd(row0_M(mode, jb, a, b), -wmul(a, jb));          // M'(0, j)
+        waveLds[lane] = CKPT ? m0 : 4 * m0 + 2;                             // (X form)
         C.bIn = waveLds;
       } else {
         if (c < nblk) {
@@ -383,9 +240,19 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         C.mail = mailbox + ((seq - 1) % kMailSlots) * 64;
       }
       const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
-      if (edge) tag_chunk<R, TV_EDGE, WIDE>(S, C, c);
-      else if (lastStrip && selRow) tag_chunk<R, TV_SEL, WIDE>(S, C, c);
-      else tag_chunk<R, TV_FAST, WIDE>(S, C, c);
+      if constexpr (CKPT) {
+        int32_t* ck = ckBase + (size_t)c * (R + 1) * BG_WAVE;
+#pragma unroll
+        for (int k = 0; k < R; ++k) ck[k * BG_WAVE] = S.Y[k];
+        ck[R * BG_WAVE] = S.topPrev;
+        if (edge) score_chunk<R, TV_EDGE, WIDE>(S, C, c);
+        else if (lastStrip && selRow) score_chunk<R, TV_SEL, WIDE>(S, C, c);
+        else score_chunk<R, TV_FAST, WIDE>(S, C, c);
+      } else {
+        if (edge) tag_chunk<R, TV_EDGE, WIDE>(S, C, c);
+        else if (lastStrip && selRow) tag_chunk<R, TV_SEL, WIDE>(S, C, c);
+        else tag_chunk<R, TV_FAST, WIDE>(S, C, c);
+      }
       // publish.  LDS mailbox: the block's ds_writes precede the counter's in this wave's LDS
       // queue.  HBM: the chunk ends with the block store and R trace stores; at vmcnt(R) the
       // block store has completed (vector memory operations complete in order).
@@ -393,7 +260,8 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       if (mailOut) {
         if (lane == 0) __hip_atomic_store(sProg + w, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
+        if constexpr (CKPT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
         if constexpr (WIDE) {
           if (lane == 0) __hip_atomic_store(gProg + gw, (uint32_t)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
@@ -406,9 +274,11 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   }
 }
 
-#define BG_TAG_INST(RR)                                            \
-  template __global__ void bg_dp_tag_kernel<RR, false>(BgDpArgs);  \
-  template __global__ void bg_dp_tag_kernel<RR, true>(BgDpArgs);
+#define BG_TAG_INST(RR)                                                   \
+  template __global__ void bg_dp_tag_kernel<RR, false, false>(BgDpArgs);  \
+  template __global__ void bg_dp_tag_kernel<RR, true, false>(BgDpArgs);   \
+  template __global__ void bg_dp_tag_kernel<RR, false, true>(BgDpArgs);   \
+  template __global__ void bg_dp_tag_kernel<RR, true, true>(BgDpArgs);
 BG_TAG_INST(2)
 BG_TAG_INST(3)
 BG_TAG_INST(4)
@@ -416,10 +286,12 @@ BG_TAG_INST(5)
 BG_TAG_INST(8)
 BG_TAG_INST(10)
 
-extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide) {
+extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt) {
   switch (R) {
-#define BG_TAG_CASE(RR) \
-    case RR: return wide ? (void*)&bg_dp_tag_kernel<RR, true> : (void*)&bg_dp_tag_kernel<RR, false>;
+#define BG_TAG_CASE(RR)                                                                   \
+    case RR:                                                                              \
+      if (ckpt) return wide ? (void*)&bg_dp_tag_kernel<RR, true, true> : (void*)&bg_dp_tag_kernel<RR, false, true>; \
+      return wide ? (void*)&bg_dp_tag_kernel<RR, true, false> : (void*)&bg_dp_tag_kernel<RR, false, false>;
     BG_TAG_CASE(2)
     BG_TAG_CASE(3)
     BG_TAG_CASE(4)

@@ -132,6 +132,7 @@ typedef struct bg_stats {
   int32_t npairs;
   int32_t wide;            /* 1: tagged kernel with each pair spread over a group of workgroups */
   int32_t workgroups;      /* DP grid size */
+  int32_t checkpoint;      /* 1: score-only DP + traceback recomputing the chunks its path crosses */
   float dp_ms;             /* last execute: DP kernel time (HIP events on the handle's stream) */
   float finish_ms;         /* last execute: end-cell + traceback kernel time */
 } bg_stats;
@@ -158,8 +159,10 @@ int bg_set_tuning(bg_aligner* h, int R, int waves);
  * Takes effect at the next bg_batch_prepare. */
 int bg_set_pipeline(bg_aligner* h, int depth);
 
-/* allow_tagged = 0 forces the mask-trace kernel where the tagged linear kernel would be used
- * (tests compare both).  Takes effect at the next bg_batch_prepare. */
+/* Kernel selection for tests and benchmarks (default 3).  Bit 0: allow the tagged linear kernel
+ * (else the mask-trace kernel); bit 1: with it, run the score-only DP and recompute the chunks
+ * the traceback crosses from checkpoints (else the tagged DP writes the full trace).  Takes
+ * effect at the next bg_batch_prepare. */
 int bg_set_kernel_options(bg_aligner* h, int allow_tagged);
 
 const char* bg_status_string(int status);

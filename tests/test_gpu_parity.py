@@ -192,14 +192,14 @@ def test_geometries_multistrip(aligner, oracle, R, W, mode, a, b):
         aligner.set_tuning(0, 0)
 
 
-@pytest.mark.parametrize("tagged", [True, False])
+@pytest.mark.parametrize("kernel", ["checkpoint", "tagged", "mask"])
 @pytest.mark.parametrize("R,W", [(2, 4), (3, 16), (4, 3), (5, 1), (5, 8), (8, 16), (10, 2), (10, 16)])
 @pytest.mark.parametrize("mode", ["semiglobal", "local", "overlap", "fitting", "global"])
-def test_geometries_linear_dna(aligner, oracle, R, W, mode, tagged):
-    """The metric-path kernels (linear gaps a >= b, DNA register profile) at every strip height,
-    tagged (tie-break tag in the score) and mask-trace variants."""
+def test_geometries_linear_dna(aligner, oracle, R, W, mode, kernel):
+    """The metric-path kernels (linear gaps a >= b, DNA register profile) at every strip height:
+    score-only DP + checkpoint traceback, tagged DP with the full trace, mask-trace DP."""
     rng = random.Random(R * 1000 + W)
-    aligner._h.set_kernel_options(tagged)
+    aligner._h.set_kernel_options(kernel != "mask", kernel == "checkpoint")
     aligner.set_tuning(R, W)
     try:
         pairs = []
@@ -208,18 +208,23 @@ def test_geometries_linear_dna(aligner, oracle, R, W, mode, tagged):
             s2 = mutate(rng, s1, DNA, 0.15)[:n2]
             pairs.append((s1, s2))
         check_batch(aligner, oracle, mode, pairs, "blosum62", -1, -2, fresh=False)
+        st = aligner.stats()
+        if mode != "local":
+            assert st["checkpoint"] == (kernel == "checkpoint") and st["tagged"] == (kernel != "mask"), st
     finally:
         aligner.set_tuning(0, 0)
         aligner._h.set_kernel_options(True)
 
 
+@pytest.mark.parametrize("ckpt", [True, False])
 @pytest.mark.parametrize("R", [0, 2, 5])
 @pytest.mark.parametrize("mode", ["semiglobal", "global", "overlap", "fitting"])
-def test_wide_pairs(aligner, oracle, mode, R):
+def test_wide_pairs(aligner, oracle, mode, R, ckpt):
     """Few long pairs: the tagged kernel spreads each pair's strips over a group of workgroups
     (global agent-scope progress counters, groups spanning XCDs); bit-exact against the oracle."""
     rng = random.Random(31 + R)
     aligner.set_tuning(R, 0)
+    aligner._h.set_kernel_options(True, ckpt)
     try:
         pairs = []
         for n1, n2 in ((5000, 4100), (4500, 3000), (4103, 900), (300, 200), (6000, 64)):
@@ -229,9 +234,11 @@ def test_wide_pairs(aligner, oracle, mode, R):
         res = check_batch(aligner, oracle, mode, pairs, "blosum62", -1, -2, fresh=False)
         st = aligner.stats()
         assert st["tagged"] == 1 and st["wide"] == 1 and st["workgroups"] > len(pairs), st
+        assert st["checkpoint"] == int(ckpt)
         assert all(r.status == 0 for r in res)
     finally:
         aligner.set_tuning(0, 0)
+        aligner._h.set_kernel_options(True)
 
 
 def test_buffer_edge_and_divergence(aligner, oracle):
