@@ -331,6 +331,13 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
     const int vg = vgprs_of(fn);
     const void* ffn = h->ckpt ? bg_finish_ck_kernel_ptr(Rc, h->mode) : bg_finish_kernel_ptr(Rc, h->affine, h->mode);
     const int fin = h->depth > 1 ? vgprs_of(ffn) : 0;
+    // LDS of one finish workgroup that must fit beside the DP's when pipelining
+    size_t finLds = 0;
+    if (h->depth > 1) {
+      int win = 0;
+      finLds = h->ckpt ? bg_finish_ck_lds_bytes(Rc, &win)
+                       : bg_finish_lds_bytes(bg_finish_window_bytes(Rc, h->affine, np, h->cus));
+    }
     const int opsPerStep = h->ckpt ? 2 * Rc + 2 : (h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12));
     const int S = maxn1 ? (int)((maxn1 + 64 * Rc - 1) / (64 * Rc)) : 1;
     const int wmax = (h->affine || h->local) ? 8 : 16;
@@ -349,10 +356,15 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
         // the code row in LDS saves per-chunk staging, unless it costs co-resident workgroups
         const size_t waves = (size_t)Wc * bg_dp_tag_wave_lds_bytes(Rc);
         const size_t row = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
-        const int wgNoRow = (int)(160 * 1024 / (128 + waves));
-        const int wgRow = (int)(160 * 1024 / (128 + waves + row));
+        const size_t ldsCu = 160 * 1024 > finLds ? 160 * 1024 - finLds : 0;
+        const int wgNoRow = (int)(ldsCu / (128 + waves));
+        const int wgRow = (int)(ldsCu / (128 + waves + row));
         rowc = wgRow >= std::min(wg, wgNoRow) && wgRow >= 1;
         wg = std::min(wg, rowc ? wgRow : wgNoRow);
+        if (wg < 1) {
+          if (!(h->tuneR && h->tuneW)) continue;
+          wg = 1;
+        }
       }
       if (wg < 1) {
         if (!(h->tuneR && h->tuneW)) continue;
