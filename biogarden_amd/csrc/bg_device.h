@@ -107,6 +107,7 @@ struct BgFinishArgs {
   const uint8_t* codes1;
   const uint8_t* codes2;
   const int32_t* profile;
+  unsigned long long* dbg;  // optional per-pair cycle counters (env BG_FINISH_TIMING)
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

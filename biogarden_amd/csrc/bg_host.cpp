@@ -110,7 +110,7 @@ struct bg_aligner {
   std::vector<int2> wgmap;
   int gridWgs = 0;
   uint32_t progWords = 0;
-  DevBuf wgmapBuf, gprogBuf;
+  DevBuf wgmapBuf, gprogBuf, dbgBuf;
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
   float dp_ms = 0.f, fin_ms = 0.f;
@@ -762,6 +762,11 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.codes1 = h->codes1.as<uint8_t>();
     F.codes2 = h->codes2.as<uint8_t>();
     F.profile = h->prof.as<int32_t>();
+    F.dbg = nullptr;
+    if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(64 * (np + 1))) {
+      F.dbg = h->dbgBuf.as<unsigned long long>();
+      BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, h->stream2));
+    }
     void* args[] = {&F};
     if (h->ckpt) {
       int win = 0;
@@ -810,6 +815,15 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   int rc = bg_synchronize(h);
   if (rc) return rc;
   const size_t np = h->plan.size();
+  if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.p && np) {
+    std::vector<unsigned long long> d(8 * np);
+    BG_HIP(hipMemcpy(d.data(), h->dbgBuf.p, 64 * np, hipMemcpyDeviceToHost));
+    double s[6] = {0, 0, 0, 0, 0, 0};
+    for (size_t p = 0; p < np; ++p)
+      for (int x = 0; x < 6; ++x) s[x] += (double)d[8 * p + x];
+    std::fprintf(stderr, "finish timing (per pair avg, cycles): walk %.0f  jump %.0f (n %.1f)  miss %.0f (n %.1f)  ops %.0f\n",
+                 s[0] / np, s[1] / np, s[2] / np, s[3] / np, s[4] / np, s[5] / np);
+  }
   h->hres.resize(np);
   uint64_t ob = 0;
   for (const BgPair& P : h->plan) ob += (uint64_t)P.n1 + P.n2;

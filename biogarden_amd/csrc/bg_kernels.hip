@@ -498,6 +498,13 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   // checkpoint mode: the window is kCkSlots recomputed chunks; sh[16+z] / sh[24+z] = strip /
   // chunk held by slot z (-1: empty); per-wave recompute areas follow the scan
   int* ckArea = scan + 2 * 256;
+  int* jscr = ckArea + (CK ? 4 * ck_wave_ints<R>() : 0);
+  // checkpoint mode: direct-mapped table (strip & 31, chunk & 31) -> (s << 20 | c << 4 | slot)
+  unsigned* ckMap = reinterpret_cast<unsigned*>(jscr);
+  if (CK) {
+    for (int x = threadIdx.x; x < 1024; x += blockDim.x) ckMap[x] = 0xFFFFFFFFu;
+    __syncthreads();
+  }
 
   const BgPair& P = F.pairs[blockIdx.x];
   const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6), NT = blockDim.x;
@@ -621,52 +628,47 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
 #pragma unroll
   for (int z = 0; z < kCkSlots; ++z) { ckS[z] = -1; ckC[z] = -1; }
   // decodes the 8x8 neighbourhood anchored at (k, l): lane (dk, dl) holds cell (k - dk, l - dl)
-  auto reanchor = [&](int ka, int la) {
-    k0 = ka; l0 = la;
-    const int kk = k0 - (lane >> 3), ll = l0 - (lane & 7);
-    if (kk <= 0 || ll <= 0) {
-      codes = kCodeBorder | ((kk == 0) ? 2 : 1);    // m_trace borders: column 0 'X', row 0 'Y'
+  // 4-bit code of cell (kk, ll) from the resident trace (window or recomputed chunks)
+  auto decode_cell = [&](int kk, int ll) -> int {
+    if (kk <= 0 || ll <= 0) return kCodeBorder | ((kk == 0) ? 2 : 1);  // column 0 'X', row 0 'Y'
+    const int vr = kk - 1;
+    const int sidx = vr / ROWS, rem = vr - sidx * ROWS, r = rem / R, q = rem - r * R;
+    const int t = ll + r, bl = t >> 5;
+    if constexpr (CK) {
+      const int cc = t >> 6;
+      const unsigned e = ckMap[((sidx & 31) << 5) | (cc & 31)];   // (s << 20 | c << 4 | slot)
+      if ((e >> 4) != (((unsigned)sidx << 16) | (unsigned)cc) || e == 0xFFFFFFFFu) return kCodeMiss;
+      const int z = (int)(e & 15);
+      const uint32_t* wp = win + (size_t)z * ck_slot_dw<R>() + (((bl & 1) * R + q) * BG_WAVE + r) * 2;
+      const uint2 v = *reinterpret_cast<const uint2*>(wp);
+      const int u = t & 31;
+      const int tg = (int)((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3;
+      return ((0x2100 >> (4 * tg)) & 3) | 12;
     } else {
-      const int vr = kk - 1;
-      const int sidx = vr / ROWS, rem = vr - sidx * ROWS, r = rem / R, q = rem - r * R;
-      const int t = ll + r, bl = t >> 5;
-      if constexpr (CK) {
-        const int cc = t >> 6;
-        int z = -1;
-#pragma unroll
-        for (int zz = 0; zz < kCkSlots; ++zz)
-          if (ckS[zz] == sidx && ckC[zz] == cc) z = zz;
-        if (z < 0) {
-          codes = kCodeMiss;
-        } else {
-          const uint32_t* wp = win + (size_t)z * ck_slot_dw<R>() + (((bl & 1) * R + q) * BG_WAVE + r) * 2;
-          const uint2 v = *reinterpret_cast<const uint2*>(wp);
-          const int u = t & 31;
-          const int tg = (int)((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3;
-          codes = ((0x2100 >> (4 * tg)) & 3) | 12;
-        }
-      } else if (sidx != curS || bl < curB0 || bl >= curB0 + curNb) {
-        codes = kCodeMiss;
+      if (sidx != curS || bl < curB0 || bl >= curB0 + curNb) return kCodeMiss;
+      const uint32_t* wp = win + (((bl - curB0) * R + q) * BG_WAVE + r) * NW;
+      const int bit = 31 - (t & 31);
+      if constexpr (AFFINE) {
+        const uint4 v = *reinterpret_cast<const uint4*>(wp);
+        return (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | (((v.z >> bit) & 1) << 2) | (((v.w >> bit) & 1) << 3);
+      } else if (F.tag) {
+        const uint2 v = *reinterpret_cast<const uint2*>(wp);  // 2-bit codes, 16 steps/word
+        const int u = t & 31;
+        const int tg = (int)((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3;
+        return ((0x2100 >> (4 * tg)) & 3) | 12;                // tag 0 'R', 2 'X', 3 'Y'
       } else {
-        const uint32_t* wp = win + (((bl - curB0) * R + q) * BG_WAVE + r) * NW;
-        const int bit = 31 - (t & 31);
-        int c;
-        if constexpr (AFFINE) {
-          const uint4 v = *reinterpret_cast<const uint4*>(wp);
-          c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | (((v.z >> bit) & 1) << 2) | (((v.w >> bit) & 1) << 3);
-        } else if (F.tag) {
-          const uint2 v = *reinterpret_cast<const uint2*>(wp);  // 2-bit codes, 16 steps/word
-          const int u = t & 31;
-          const int tg = (int)((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3;
-          c = ((0x2100 >> (4 * tg)) & 3) | 12;                 // tag 0 'R', 2 'X', 3 'Y'
-        } else {
-          const uint2 v = *reinterpret_cast<const uint2*>(wp);
-          c = (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | 12;
-        }
-        codes = c;
+        const uint2 v = *reinterpret_cast<const uint2*>(wp);
+        return (((v.x >> bit) & 1) << 1) | ((v.y >> bit) & 1) | 12;
       }
     }
   };
+  // decodes the 8x8 neighbourhood anchored at (k, l): lane (dk, dl) holds cell (k - dk, l - dl)
+  auto reanchor = [&](int ka, int la) {
+    k0 = ka; l0 = la;
+    codes = decode_cell(k0 - (lane >> 3), l0 - (lane & 7));
+  };
+  u64 tJump = 0, tMiss = 0, nJump = 0, nMiss = 0;        // BG_FINISH_TIMING instrumentation
+  const u64 tWalk0 = __builtin_readcyclecounter();
   for (;;) {
     int reqS = -1, reqB0 = 0, done = 0;
     if (wid == 0) {
@@ -726,6 +728,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
               l -= (mvP != 2);
             }
             state = mvIn == 2 ? 1 : (mvIn == 3 ? 2 : 0);
+            ++nJump;
             continue;
           }
         } else {
@@ -841,6 +844,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     __syncthreads();
     done = sh[6];
     if (done) break;
+    const u64 tm0 = __builtin_readcyclecounter();
+    ++nMiss;
     reqS = uni(sh[4]);
     reqB0 = uni(sh[5]);
     if constexpr (CK) {
@@ -861,9 +866,18 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                            ckArea + wid * ck_wave_ints<R>(), lane);
       for (int x = 0; x < nl; ++x) {
         const int z = (ckNext + x) % kCkSlots;
+        int oldS = -1, oldC = -1;
 #pragma unroll
         for (int zz = 0; zz < kCkSlots; ++zz)
-          if (zz == z) { ckS[zz] = reqS; ckC[zz] = list[x]; }
+          if (zz == z) { oldS = ckS[zz]; oldC = ckC[zz]; ckS[zz] = reqS; ckC[zz] = list[x]; }
+        if (tid == 0) {
+          if (oldS >= 0) {
+            unsigned& oe = ckMap[((oldS & 31) << 5) | (oldC & 31)];
+            if ((oe & 15) == (unsigned)z) oe = 0xFFFFFFFFu;
+          }
+          ckMap[((reqS & 31) << 5) | (list[x] & 31)] =
+              ((unsigned)reqS << 20) | ((unsigned)list[x] << 4) | (unsigned)z;
+        }
       }
       ckNext = (ckNext + nl) % kCkSlots;
       k0 = -1000000;
@@ -890,6 +904,12 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       k0 = -1000000;                                   // decode the neighbourhood again
     }
     __syncthreads();
+    tMiss += __builtin_readcyclecounter() - tm0;
+  }
+  if (F.dbg && tid == 0) {
+    u64* d = F.dbg + (size_t)P.index * 8;
+    d[0] = __builtin_readcyclecounter() - tWalk0;
+    d[1] = tJump; d[2] = nJump; d[3] = tMiss; d[4] = nMiss; d[5] = (u64)ncore;
   }
 
   // ---------------- semiglobal prefix gaps (:416-428); every wave knows k, l through sh
@@ -1070,7 +1090,7 @@ extern "C" size_t bg_finish_ck_lds_bytes(int R, int* win_bytes) {
     default: slot = ck_slot_dw<10>(); area = ck_wave_ints<10>(); break;
   }
   *win_bytes = kCkSlots * slot * 4;
-  return (size_t)*win_bytes + 64 * 4 + 2 * 256 * 4 + 4 * (size_t)area * 4;
+  return (size_t)*win_bytes + 64 * 4 + 2 * 256 * 4 + 4 * (size_t)area * 4 + 4 * 1024;  // + chunk map
 }
 
 template <int R, bool AF>
