@@ -305,11 +305,12 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
 // Geometry planner (DESIGN.md "Geometry").  For each strip height R and wave count W the strip
 // pipeline of the largest pair is simulated phase by phase (a phase = 64 anti-diagonal steps;
 // strip s starts two phases after strip s-1 and after its wave finished strip s-W).  A phase
-// with a active waves per SIMD costs 64 * ops_per_step * a * (4.0 + 0.6 / a) cycles: ~4 cycles
-// per VALU instruction when the SIMD is shared (tools/micro/tag_step.hip), a little more for a
-// lone wave.  Workgroups per CU are bounded by waves (32 per CU) and by VGPRs; with the two-slot
-// pipeline a finish workgroup must still fit beside them (one wave per SIMD).  Ties within 1 %
-// go to more waves per SIMD.
+// with a active waves per SIMD costs 64 * ops_per_step * a * (4.0 + 3.0 / a) cycles: ~4 cycles
+// per VALU instruction when enough waves share the SIMD (tools/micro/tag_step.hip), and the
+// measured ~5.6 at two waves per SIMD (PMC, profiles/r01/pmc_summary_ckptR10W8.json), where the
+// per-step LDS and memory latencies are no longer hidden.  Workgroups per CU are bounded by
+// waves (32 per CU), VGPRs and LDS; with the two-slot pipeline a finish workgroup must still fit
+// beside them.  Ties within 1 % go to more waves per SIMD.
 static int vgprs_of(const void* fn) {
   hipFuncAttributes at;
   if (!fn || hipFuncGetAttributes(&at, fn) != hipSuccess || at.numRegs <= 0) return 128;
@@ -386,7 +387,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
       for (int p = 0; p < P; ++p) {
         A += diff[p];
         const int a = std::max(1, (A * wg + 3) / 4);
-        T += 64.0 * opsPerStep * a * (4.0 + 0.6 / a);
+        T += 64.0 * opsPerStep * a * (4.0 + 3.0 / a);
       }
       const double rounds = std::ceil((double)np / ((double)h->cus * wg));
       T *= rounds;

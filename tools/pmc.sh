@@ -9,7 +9,7 @@ IFS=';' read -ra P <<< "${PASSES}"
 i=0
 for grp in "${P[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${grp//,/ } -d $OUT/p$i -o run --output-format csv -- python3 bench.py --no-cpu --steps 2 --warmup 0 --pipeline 1 ${BENCH_ARGS} > $OUT/p$i.json 2> $OUT/p$i.err || { tail -20 $OUT/p$i.err; exit 1; }
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc ${grp//,/ } -d $OUT/p$i -o run --output-format csv -- python3 bench.py --no-cpu --steps 2 --warmup 0 --pipeline 1 ${BENCH_ARGS} > $OUT/p$i.json 2> $OUT/p$i.err || { tail -3 $OUT/p$i.err; echo "pass $i failed: $grp"; continue; }
   echo "pass $i: $grp ok"
 done
 python3 tools/pmc_summary.py $OUT
