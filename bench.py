@@ -81,8 +81,9 @@ def main():
     ap.add_argument("--extend", type=int, default=-2)
     ap.add_argument("--R", type=int, default=0)
     ap.add_argument("--waves", type=int, default=0)
-    ap.add_argument("--pipeline", type=int, default=2,
-                    help="2: traceback of step k overlaps the DP of step k+1 (two HIP streams)")
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="slots: >= 2 lets the traceback of step k overlap the DP of step k+1 "
+                         "(two HIP streams); 3 absorbs traceback times that vary around the DP's")
     ap.add_argument("--cpu-pairs", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gather", action="store_true")

@@ -74,7 +74,7 @@ struct bg_aligner {
   hipStream_t stream2 = nullptr;   // end cell + traceback kernels
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
   DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
-  Slot slot[2];
+  Slot slot[3];
   int depth = 2;                   // pipeline depth (1 or 2 slots)
   int execCount = 0;
   int lastSlot = 0;
@@ -230,7 +230,7 @@ extern "C" int bg_set_kernel_options(bg_aligner* h, int allow_tagged) {
 }
 
 extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
-  if (!h || depth < 1 || depth > 2) return BG_E_ARG;
+  if (!h || depth < 1 || depth > 3) return BG_E_ARG;
   if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream2) != hipSuccess)
     return BG_E_HIP;
@@ -323,7 +323,8 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   const size_t np = std::max<size_t>(ncomp, 1);
   const int NC = (int)(maxn2 / 64 + 2);
   double best = 1e300;
-  int bestWps = 0;
+  struct Cand { double T; int R, W, wps, row; };
+  std::vector<Cand> cands;
   std::vector<int> start, end, diff;
   for (int Rc : cand) {
     if (h->tuneR && Rc != h->tuneR) continue;
@@ -358,8 +359,8 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
         const size_t waves = (size_t)Wc * bg_dp_tag_wave_lds_bytes(Rc);
         const size_t row = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
         const size_t ldsCu = 160 * 1024 > finLds ? 160 * 1024 - finLds : 0;
-        const int wgNoRow = (int)(ldsCu / (128 + waves));
-        const int wgRow = (int)(ldsCu / (128 + waves + row));
+        const int wgNoRow = (int)(ldsCu / (640 + waves));
+        const int wgRow = (int)(ldsCu / (640 + waves + row));
         rowc = wgRow >= std::min(wg, wgNoRow) && wgRow >= 1;
         wg = std::min(wg, rowc ? wgRow : wgNoRow);
         if (wg < 1) {
@@ -392,14 +393,23 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
       const double rounds = std::ceil((double)np / ((double)h->cus * wg));
       T *= rounds;
       const int wpsAll = wps * wg;
-      if (T < best * 0.99 || (T < best * 1.01 && wpsAll > bestWps)) {
-        if (T < best) best = T;
-        *Rout = Rc;
-        *Wout = Wc;
-        bestWps = wpsAll;
-        h->tagRow = rowc ? 1 : 0;
-      }
+      cands.push_back({T, Rc, Wc, wpsAll, rowc ? 1 : 0});
+      best = std::min(best, T);
     }
+  }
+  // within 5 % of the best estimate: taller strips (fewer per-step overhead ops per cell; the
+  // pipeline tail the model charges for is filled by the overlapped traceback), then more waves
+  // per SIMD, then the estimate
+  const Cand* pick = nullptr;
+  for (const Cand& c : cands) {
+    if (c.T > best * 1.05) continue;
+    if (!pick || c.R > pick->R || (c.R == pick->R && (c.wps > pick->wps || (c.wps == pick->wps && c.T < pick->T))))
+      pick = &c;
+  }
+  if (pick) {
+    *Rout = pick->R;
+    *Wout = pick->W;
+    h->tagRow = pick->row;
   }
 }
 
@@ -509,12 +519,12 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   if (h->tag) {
     // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
     // boundary block, output ring, profile entries, the current chunk's codes and the mailbox
-    h->progOff = 0;
-    h->codesOff = 128;
+    h->progOff = 0;                  // counters + shared dummy ring: 640 B
+    h->codesOff = 640;
     const size_t waves = (size_t)W * bg_dp_tag_wave_lds_bytes(R);
     const size_t row = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
-    h->codesInLds = (h->tagRow && 128 + row + waves <= 160 * 1024) ? 1 : 0;
-    h->auxLdsOff = (int)(128 + (h->codesInLds ? row : 0));
+    h->codesInLds = (h->tagRow && 640 + row + waves <= 160 * 1024) ? 1 : 0;
+    h->auxLdsOff = (int)(640 + (h->codesInLds ? row : 0));
     lds = h->auxLdsOff + waves;
     // WIDE: one workgroup (one wave per SIMD) per CU — claim over half of the CU's LDS so the
     // dispatcher cannot stack a group's workgroups on one CU

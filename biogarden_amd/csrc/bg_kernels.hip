@@ -419,7 +419,10 @@ constexpr int kCodeMiss = 32, kCodeBorder = 16;
 // tagged step (tag_chunk<KIND_RECOMP>, the same arithmetic as the tagged forward kernel) and
 // leaves the chunk's 2-bit trace in an LDS slot laid out like the HBM trace of two 32-step
 // blocks: [h][row k][lane] x uint2.
-constexpr int kCkSlots = 8;
+// resident recomputed chunks: 8, or 6 for tall strips (keeps the finish workgroup's LDS small
+// enough to run beside the DP's)
+template <int R>
+__host__ __device__ constexpr int ck_slots() { return R >= 8 ? 6 : 8; }
 template <int R>
 __host__ __device__ constexpr int ck_slot_dw() { return 2 * R * BG_WAVE * 2; }
 template <int R>
@@ -495,7 +498,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   uint32_t* win = reinterpret_cast<uint32_t*>(smem);
   int* sh = reinterpret_cast<int*>(smem + F.win_bytes);  // 64 ints of block-shared scalars
   int* scan = sh + 64;                                 // 2 x 256 ints
-  // checkpoint mode: the window is kCkSlots recomputed chunks; sh[16+z] / sh[24+z] = strip /
+  // checkpoint mode: the window is ck_slots<R>() recomputed chunks; sh[16+z] / sh[24+z] = strip /
   // chunk held by slot z (-1: empty); per-wave recompute areas follow the scan
   int* ckArea = scan + 2 * 256;
   int* jscr = ckArea + (CK ? 4 * ck_wave_ints<R>() : 0);
@@ -623,6 +626,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     for (int c = 0; c < 16; ++c) v |= (u64)((c & 8) ? 0 : ((3u << 2) | 2)) << (4 * c);
     return v;
   }();
+  constexpr int kCkSlots = ck_slots<R>();
   int ckS[kCkSlots], ckC[kCkSlots];                  // checkpoint mode: resident chunks
   int ckNext = 0;                                    // next slot to fill (FIFO)
 #pragma unroll
@@ -1080,16 +1084,16 @@ extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode) {
 }
 // LDS of the checkpoint finish kernel: chunk slots, scalars + scan, 4 recompute areas
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int* win_bytes) {
-  int slot = 0, area = 0;
+  int slot = 0, area = 0, nslot = 8;
   switch (R) {
-    case 2: slot = ck_slot_dw<2>(); area = ck_wave_ints<2>(); break;
-    case 3: slot = ck_slot_dw<3>(); area = ck_wave_ints<3>(); break;
-    case 4: slot = ck_slot_dw<4>(); area = ck_wave_ints<4>(); break;
-    case 5: slot = ck_slot_dw<5>(); area = ck_wave_ints<5>(); break;
-    case 8: slot = ck_slot_dw<8>(); area = ck_wave_ints<8>(); break;
-    default: slot = ck_slot_dw<10>(); area = ck_wave_ints<10>(); break;
+    case 2: slot = ck_slot_dw<2>(); area = ck_wave_ints<2>(); nslot = ck_slots<2>(); break;
+    case 3: slot = ck_slot_dw<3>(); area = ck_wave_ints<3>(); nslot = ck_slots<3>(); break;
+    case 4: slot = ck_slot_dw<4>(); area = ck_wave_ints<4>(); nslot = ck_slots<4>(); break;
+    case 5: slot = ck_slot_dw<5>(); area = ck_wave_ints<5>(); nslot = ck_slots<5>(); break;
+    case 8: slot = ck_slot_dw<8>(); area = ck_wave_ints<8>(); nslot = ck_slots<8>(); break;
+    default: slot = ck_slot_dw<10>(); area = ck_wave_ints<10>(); nslot = ck_slots<10>(); break;
   }
-  *win_bytes = kCkSlots * slot * 4;
+  *win_bytes = nslot * slot * 4;
   return (size_t)*win_bytes + 64 * 4 + 2 * 256 * 4 + 4 * (size_t)area * 4 + 4 * 1024;  // + chunk map
 }
 

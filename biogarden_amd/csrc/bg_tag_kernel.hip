@@ -38,7 +38,8 @@
 using namespace bgk;
 
 // LDS layout (bytes from the dynamic base; the host sizes it in bg_host.cpp):
-//   16 produced + 16 consumed counters (128 B, @prog_off) | the pair's scaled code row when it
+//   16 produced + 16 consumed counters + a 128-int shared dummy ring (640 B, @prog_off) | the
+//   pair's scaled code row when it
 //   fits (@codes_off, u16, 64 zeros before it, NC + 2 chunks) | per wave @aux_lds_off: 64-int
 //   boundary block, 256-int output ring, 4 codes x 64 lanes x RW-dword profile entries, 192 u16
 //   scaled codes of the current chunk (columns t0-64 .. t0+127), 4 x 64-int mailbox.
@@ -53,7 +54,8 @@ using namespace bgk;
 // and the progress counters live in global memory (A.gprog + P.prog_off), written and polled
 // with agent-scope atomics like the boundary rows, so the group may span XCDs.  All workgroups
 // of a group are resident together (the host caps the group at the CU count).
-constexpr int kTagWaveInts = 64 + 256;
+constexpr int kTagWaveInts = 64 + 128;   // boundary block + output ring (last-strip lanes below
+                                         // row n1 write a workgroup-shared dummy ring)
 constexpr int kTagStageU16 = 192;
 constexpr int kMailSlots = 4;   // boundary blocks in flight between two waves of a workgroup
 
@@ -82,6 +84,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   }
   int* sProg = reinterpret_cast<int*>(smem + A.prog_off);   // blocks produced (per wave)
   int* sCons = sProg + 16;                                   // chunks consumed (per wave)
+  int* dummyRing = sProg + 32;                               // 128 ints, shared garbage
   if (threadIdx.x < 32) sProg[threadIdx.x] = 0;
   // the pair's whole scaled code row, when it fits (A.codes_in_lds): 64 zero entries before it
   // and zeros past n2 up to (NC + 2) chunks; else codes are staged per wave and chunk
@@ -152,7 +155,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     const int olane = lastStrip ? lastRow / R : BG_WAVE - 1;
     C.orow = lastStrip ? lastRow % R : R - 1;
     const bool selRow = C.orow != R - 1;
-    C.oLane = C.ring + (lane <= olane ? 64 : 192) - lane;
+    C.oLane = (lane <= olane ? C.ring : dummyRing) + 64 - lane;
     C.trace = A.trace + P.trace_off / 4 + (size_t)s * stripDw;
     C.bndOut = A.bndM + P.bnd_off + (size_t)s * NC * BG_CHUNK;
     // strip s+1 on the next wave of this workgroup in this round: hand blocks over in LDS
