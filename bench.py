@@ -178,7 +178,11 @@ def main():
     ok_status = all(r["status"] == 0 for rr in results0 for r in rr)
 
     # ---- roofline of the DP kernel (algorithmic bytes per launch / event-timed duration)
-    bytes_per_cell = 0.25 if st["affine"] == 0 else 0.5
+    if st["checkpoint"]:
+        # score-only DP: per lane and 64-step chunk R + 1 checkpoint ints, per strip its last row
+        bytes_per_cell = (4.0 * (st["R"] + 1) + 4.0) / (64.0 * st["R"])
+    else:
+        bytes_per_cell = 0.25 if st["affine"] == 0 else 0.5    # the 2-bit (4-bit) trace
     algo_bytes = cells * bytes_per_cell + st["residue_bytes"]
     achieved = algo_bytes / (dp_ms * 1e-3) / 1e9 if dp_ms > 0 else 0.0
     workload = "semiglobal_%dx%dx%d_blosum62_o%d_e%d" % (args.pairs, args.len1, args.len2,
@@ -231,15 +235,16 @@ def main():
                    "len2": args.len2, "mode": args.mode, "scoring": "blosum62",
                    "gap_open": args.open, "gap_extend": args.extend,
                    "kernel": {"R": st["R"], "waves": st["waves"], "affine": st["affine"],
-                              "tagged": st["tagged"], "dna_profile": st["dna"],
-                              "pipeline": args.pipeline},
+                              "tagged": st["tagged"], "checkpoint": st["checkpoint"],
+                              "dna_profile": st["dna"], "pipeline": args.pipeline},
                    "parallelism": "dp%d (independent pairs per rank)" % world},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
                      "algorithmic_bytes_per_launch": int(algo_bytes),
                      "traffic_source": ("profiles/pmc_%s.json" % workload) if traffic else None,
-                     "kernel": "bg_dp_tag_kernel" if st["tagged"] else "bg_dp_kernel",
+                     "kernel": ("bg_dp_tag_kernel<ckpt>" if st["checkpoint"] else "bg_dp_tag_kernel")
+                               if st["tagged"] else "bg_dp_kernel",
                      "kernel_ms": round(dp_ms, 4), "finish_ms": round(fin_ms, 4),
                      "valu": valu},
         "cpu_baseline": cpu,
