@@ -136,11 +136,14 @@ class Handle:
     def set_tuning(self, R=0, waves=0):
         check(lib().bg_set_tuning(self._p, R, waves))
 
-    def set_kernel_options(self, allow_tagged=True, checkpoint=True):
+    def set_kernel_options(self, allow_tagged=True, checkpoint=True, affine_checkpoint=True):
         """allow_tagged: tagged linear kernel (else mask trace); checkpoint: score-only DP with
-        the traceback recomputing the chunks it crosses (else the full trace is written)."""
+        the traceback recomputing the chunks it crosses (else the full trace is written);
+        affine_checkpoint: the same for affine gaps / local mode / > 4 symbols (else the
+        mask-trace kernel)."""
         check(lib().bg_set_kernel_options(self._p, (1 if allow_tagged else 0) |
-                                          (2 if (allow_tagged and checkpoint) else 0)))
+                                          (2 if (allow_tagged and checkpoint) else 0) |
+                                          (4 if affine_checkpoint else 0)))
 
     def set_pipeline(self, depth):
         check(lib().bg_set_pipeline(self._p, depth))

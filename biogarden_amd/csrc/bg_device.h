@@ -108,6 +108,12 @@ struct BgFinishArgs {
   const uint8_t* codes2;
   const int32_t* profile;
   unsigned long long* dbg;  // optional per-pair cycle counters (env BG_FINISH_TIMING)
+  // affine / local checkpoint traceback (bg_aff_kernel.hip): X boundary rows, alphabet size
+  // (per-lane profile entries) and the ints of one wave's recompute area
+  const int32_t* bndX;
+  int32_t kdim;
+  int32_t area_ints;
+  int32_t flags;           // bit 0: affine walk without pointer jumping (experiments, BG_NO_JUMP)
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

@@ -29,6 +29,11 @@ extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes(int win_bytes);
 extern "C" int bg_finish_window_bytes(int R, int affine, size_t npairs, int cus);
 extern "C" void* bg_export_kernel_ptr();
+extern "C" void* bg_dp_aff_kernel_ptr(int R, int local);
+extern "C" int bg_dp_aff_head_bytes(void);
+extern "C" int bg_dp_aff_wave_lds_bytes(int R, int K);
+extern "C" void* bg_finish_ack_kernel_ptr(int R, int mode);
+extern "C" size_t bg_finish_ack_lds_bytes(int R, int K, int local, int* win_bytes, int* area_ints);
 
 #include "bg_tables.inc"
 
@@ -98,7 +103,10 @@ struct bg_aligner {
   int R = 8, W = 1, affine = 0, local = 0, dna = 1, kdim = 0, tag = 0;
   int allowTag = 1;
   int allowCkpt = 1;
+  int allowAck = 1;
   int ckpt = 0;                    // tagged path: score-only DP + checkpoint traceback
+  int ack = 0;                     // affine / local path: score-only DP (bg_aff_kernel.hip) +
+                                   // traceback over recomputed full-trace chunks
   size_t lds = 0;
   int progOff = 256;
   int codesOff = 320;
@@ -224,6 +232,7 @@ extern "C" int bg_set_kernel_options(bg_aligner* h, int allow_tagged) {
   if (!h) return BG_E_ARG;
   h->allowTag = (allow_tagged & 1) ? 1 : 0;
   h->allowCkpt = (allow_tagged & 2) ? 1 : 0;
+  h->allowAck = (allow_tagged & 4) ? 1 : 0;
   h->prepared = false;
   h->executed = false;
   return BG_OK;
@@ -317,6 +326,26 @@ static int vgprs_of(const void* fn) {
   return (at.numRegs + 7) / 8 * 8;
 }
 
+// DP and finish kernels of the prepared family at strip height R (nullptr: R not built)
+static void* dp_fn(const bg_aligner* h, int R) {
+  if (h->tag) return bg_dp_kernel_tag_ptr(R, 0, h->ckpt);
+  if (h->ack) return bg_dp_aff_kernel_ptr(R, h->local);
+  return bg_dp_kernel_ptr(R, h->affine, h->local, h->dna);
+}
+static void* fin_fn(const bg_aligner* h, int R) {
+  if (h->ack) return bg_finish_ack_kernel_ptr(R, h->mode);
+  if (h->ckpt) return bg_finish_ck_kernel_ptr(R, h->mode);
+  return bg_finish_kernel_ptr(R, h->affine, h->mode);
+}
+// LDS of one finish workgroup (and the window / recompute-area sizes it launches with)
+static size_t fin_lds(const bg_aligner* h, int R, size_t np, int* win, int* area) {
+  *area = 0;
+  if (h->ack) return bg_finish_ack_lds_bytes(R, h->kdim, h->local, win, area);
+  if (h->ckpt) return bg_finish_ck_lds_bytes(R, win);
+  *win = bg_finish_window_bytes(R, h->affine, np, h->cus);
+  return bg_finish_lds_bytes(*win);
+}
+
 static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncomp, int* Rout,
                           int* Wout) {
   const int cand[] = {2, 3, 4, 5, 8, 10};
@@ -328,21 +357,21 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   std::vector<int> start, end, diff;
   for (int Rc : cand) {
     if (h->tuneR && Rc != h->tuneR) continue;
-    if (!(h->tag ? bg_dp_kernel_tag_ptr(Rc, 0, h->ckpt) != nullptr : bg_dp_has_R(Rc, h->affine, h->local, h->dna))) continue;
-    const void* fn = h->tag ? bg_dp_kernel_tag_ptr(Rc, 0, h->ckpt) : bg_dp_kernel_ptr(Rc, h->affine, h->local, h->dna);
+    const void* fn = dp_fn(h, Rc);
+    if (!fn) continue;
     const int vg = vgprs_of(fn);
-    const void* ffn = h->ckpt ? bg_finish_ck_kernel_ptr(Rc, h->mode) : bg_finish_kernel_ptr(Rc, h->affine, h->mode);
-    const int fin = h->depth > 1 ? vgprs_of(ffn) : 0;
+    const int fin = h->depth > 1 ? vgprs_of(fin_fn(h, Rc)) : 0;
     // LDS of one finish workgroup that must fit beside the DP's when pipelining
     size_t finLds = 0;
-    if (h->depth > 1) {
-      int win = 0;
-      finLds = h->ckpt ? bg_finish_ck_lds_bytes(Rc, &win)
-                       : bg_finish_lds_bytes(bg_finish_window_bytes(Rc, h->affine, np, h->cus));
+    if (h->depth > 1 || h->ack) {
+      int win = 0, area = 0;
+      finLds = fin_lds(h, Rc, np, &win, &area);
     }
-    const int opsPerStep = h->ckpt ? 2 * Rc + 2 : (h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12));
+    const size_t finLdsRes = h->depth > 1 ? finLds : 0;   // must fit beside the DP's
+    const int opsPerStep = h->ack ? (h->local ? 8 * Rc + 4 : 6 * Rc + 4)
+                         : h->ckpt ? 2 * Rc + 2 : (h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12));
     const int S = maxn1 ? (int)((maxn1 + 64 * Rc - 1) / (64 * Rc)) : 1;
-    const int wmax = (h->affine || h->local) ? 8 : 16;
+    const int wmax = (!h->ack && (h->affine || h->local)) ? 8 : 16;
     for (int Wc = 1; Wc <= wmax; ++Wc) {
       if (h->tuneW && Wc != h->tuneW) continue;
       if (Wc > S && !h->tuneW) continue;
@@ -358,7 +387,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
         // the code row in LDS saves per-chunk staging, unless it costs co-resident workgroups
         const size_t waves = (size_t)Wc * bg_dp_tag_wave_lds_bytes(Rc);
         const size_t row = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
-        const size_t ldsCu = 160 * 1024 > finLds ? 160 * 1024 - finLds : 0;
+        const size_t ldsCu = 160 * 1024 > finLdsRes ? 160 * 1024 - finLdsRes : 0;
         const int wgNoRow = (int)(ldsCu / (640 + waves));
         const int wgRow = (int)(ldsCu / (640 + waves + row));
         rowc = wgRow >= std::min(wg, wgNoRow) && wgRow >= 1;
@@ -367,6 +396,12 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
           if (!(h->tuneR && h->tuneW)) continue;
           wg = 1;
         }
+      }
+      if (h->ack) {
+        const size_t ldsCu = 160 * 1024 > finLdsRes ? 160 * 1024 - finLdsRes : 0;
+        const size_t one = bg_dp_aff_head_bytes() + (size_t)Wc * bg_dp_aff_wave_lds_bytes(Rc, h->kdim);
+        if (one > 160 * 1024) continue;
+        wg = std::min(wg, (int)(ldsCu / one));
       }
       if (wg < 1) {
         if (!(h->tuneR && h->tuneW)) continue;
@@ -392,6 +427,14 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
       }
       const double rounds = std::ceil((double)np / ((double)h->cus * wg));
       T *= rounds;
+      if (h->ack) {
+        // the traceback recomputes the chunks its path crosses: per pair ~ (600 + 8R^2) cycles
+        // per row of walk and recomputation (BG_FINISH_TIMING, C2 / C5), with as many pairs in
+        // flight per CU as the finish workgroup's LDS allows
+        const double fwg = std::max(1.0, std::floor(160.0 * 1024 / (double)std::max<size_t>(finLds, 1)));
+        const double frounds = std::ceil((double)np / ((double)h->cus * fwg));
+        T += frounds * (600.0 + 8.0 * Rc * Rc) * (double)(maxn1 + maxn2) * 0.5;
+      }
       const int wpsAll = wps * wg;
       cands.push_back({T, Rc, Wc, wpsAll, rowc ? 1 : 0});
       best = std::min(best, T);
@@ -508,6 +551,17 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
       }
   h->tag = tagOK ? 1 : 0;
   h->ckpt = (h->tag && h->allowCkpt) ? 1 : 0;
+  // affine / local score-only kernel (bg_aff_common.h): int8 profile entries S - 2a (local
+  // S - a); values, and the finite -inf drifting by e = b - a per step, far from wrapping
+  bool ackOK = !h->tag && h->allowAck && bound < 268435456.0 &&
+               std::abs((double)b - (double)a) * ((double)maxn1 + (double)maxn2 + 2.0) < 268435456.0;
+  for (int q = 0; q < 32 && ackOK; ++q)
+    for (int c = 0; c < 32 && ackOK; ++c)
+      if (present[q] && present[c]) {
+        const int64_t v = (int64_t)sc->table[q * 32 + c] - (mode == BG_LOCAL ? 1 : 2) * (int64_t)a;
+        if (v < -128 || v > 127) ackOK = false;
+      }
+  h->ack = ackOK ? 1 : 0;
 
   // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair, or a group
   // of workgroups per pair in the tagged kernel's WIDE mode)
@@ -529,6 +583,18 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     // WIDE: one workgroup (one wave per SIMD) per CU — claim over half of the CU's LDS so the
     // dispatcher cannot stack a group's workgroups on one CU
     if (h->wide) lds = std::max<size_t>(lds, 80 * 1024 + 64);
+  } else if (h->ack) {
+    // affine kernel (bg_aff_kernel.hip): counters + dummy ring, then per wave the (M, X)
+    // boundary block, output ring, profile entries, chunk codes and mailbox
+    h->progOff = 0;
+    h->codesOff = 0;
+    h->codesInLds = 0;
+    h->auxLdsOff = bg_dp_aff_head_bytes();
+    for (;;) {
+      lds = h->auxLdsOff + (size_t)W * bg_dp_aff_wave_lds_bytes(R, h->kdim);
+      if (lds <= 160 * 1024 || W == 1) break;
+      --W;
+    }
   } else {
     lds = 256;               // lut (+ int16 table and per-wave profiles on the LDS path)
     if (!h->dna) {
@@ -583,6 +649,8 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     P.trace_off = tro;
     if (h->ckpt)   // checkpoints: R + 1 ints per lane per chunk
       tro += round_up((uint64_t)P.nstrips * P.nc * (R + 1) * BG_WAVE * 4, 256);
+    else if (h->ack)   // checkpoints: 2R + 2 ints per lane per chunk
+      tro += round_up((uint64_t)P.nstrips * P.nc * (2 * R + 2) * BG_WAVE * 4, 256);
     else
       tro += round_up((uint64_t)P.nstrips * P.nc * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE * 4, 256);
     P.bnd_off = bo;
@@ -601,7 +669,7 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     h->plan.push_back(P);
   }
   h->traceBytes = tro;
-  h->bndBytes = bo * 4 * (h->affine ? 2 : 1);
+  h->bndBytes = bo * 4 * ((h->affine || h->ack) ? 2 : 1);
   h->resBytes = o1 + o2;
 
   // ---- device memory
@@ -615,7 +683,7 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   for (int z = 0; z < h->depth; ++z) {
     Slot& S = h->slot[z];
     if (!S.trace.ensure(tro + 256) || !S.bndM.ensure(bo * 4 + 256) ||
-        !S.bndX.ensure(h->affine ? bo * 4 + 256 : 256) || !S.aux.ensure(ao * 4 + 256) ||
+        !S.bndX.ensure((h->affine || h->ack) ? bo * 4 + 256 : 256) || !S.aux.ensure(ao * 4 + 256) ||
         !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) ||
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)))
       return BG_E_NOMEM;
@@ -632,10 +700,17 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   for (int x = 0; x < 256; ++x) {
     const uint8_t c = sc->code[x];
     const int d = (c < 32 && dense[c] >= 0) ? dense[c] : 0;
-    lut[x] = (uint8_t)(h->dna ? d * 8 : d);
+    lut[x] = (uint8_t)((h->dna && !h->ack) ? d * 8 : d);
   }
   std::vector<int32_t> prof(512, 0);
-  if (h->dna) {
+  if (h->ack) {
+    int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
+    const int mult = mode == BG_LOCAL ? 1 : 2;
+    for (int q = 0; q < 32; ++q)
+      for (int c = 0; c < 32; ++c)
+        if (dense[q] >= 0 && dense[c] >= 0)
+          t16[dense[q] * 32 + dense[c]] = (int16_t)(sc->table[q * 32 + c] - mult * a);
+  } else if (h->dna) {
     for (int q = 0; q < 32; ++q) {
       if (dense[q] < 0) continue;
       uint32_t packed = 0;
@@ -717,7 +792,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[0], h->stream));
   if (np) {
-    void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : bg_dp_kernel_ptr(h->R, h->affine, h->local, h->dna);
+    void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : dp_fn(h, h->R);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
     A.pairs = h->pairs.as<BgPair>();
@@ -774,12 +849,26 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.codes2 = h->codes2.as<uint8_t>();
     F.profile = h->prof.as<int32_t>();
     F.dbg = nullptr;
+    F.bndX = S.bndX.as<int32_t>();
+    F.kdim = h->kdim;
+    F.area_ints = 0;
+    F.flags = std::getenv("BG_NO_JUMP") ? 1 : 0;
     if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(64 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, h->stream2));
     }
     void* args[] = {&F};
-    if (h->ckpt) {
+    if (h->ack) {
+      int win = 0, area = 0;
+      const size_t lds = bg_finish_ack_lds_bytes(h->R, h->kdim, h->local, &win, &area);
+      F.win_bytes = win;
+      F.area_ints = area;
+      F.tag = 2;
+      F.affine = 1;
+      void* ffn = bg_finish_ack_kernel_ptr(h->R, h->mode);
+      if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(256), args, lds, h->stream2));
+    } else if (h->ckpt) {
       int win = 0;
       const size_t lds = bg_finish_ck_lds_bytes(h->R, &win);
       F.win_bytes = win;
@@ -912,7 +1001,7 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->wide = h->wide;
   o->workgroups = h->gridWgs;
   o->tagged = h->tag;
-  o->checkpoint = h->ckpt;
+  o->checkpoint = h->ckpt || h->ack;
   o->dna = h->dna;
   o->local = h->local;
   o->npairs = (int32_t)h->npairs;

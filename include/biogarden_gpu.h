@@ -159,10 +159,11 @@ int bg_set_tuning(bg_aligner* h, int R, int waves);
  * Takes effect at the next bg_batch_prepare. */
 int bg_set_pipeline(bg_aligner* h, int depth);
 
-/* Kernel selection for tests and benchmarks (default 3).  Bit 0: allow the tagged linear kernel
+/* Kernel selection for tests and benchmarks (default 7).  Bit 0: allow the tagged linear kernel
  * (else the mask-trace kernel); bit 1: with it, run the score-only DP and recompute the chunks
- * the traceback crosses from checkpoints (else the tagged DP writes the full trace).  Takes
- * effect at the next bg_batch_prepare. */
+ * the traceback crosses from checkpoints (else the tagged DP writes the full trace); bit 2: the
+ * same score-only DP + recomputing traceback for affine gaps, local mode and alphabets of more
+ * than four symbols (else the mask-trace kernel).  Takes effect at the next bg_batch_prepare. */
 int bg_set_kernel_options(bg_aligner* h, int allow_tagged);
 
 const char* bg_status_string(int status);

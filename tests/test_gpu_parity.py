@@ -199,7 +199,7 @@ def test_geometries_linear_dna(aligner, oracle, R, W, mode, kernel):
     """The metric-path kernels (linear gaps a >= b, DNA register profile) at every strip height:
     score-only DP + checkpoint traceback, tagged DP with the full trace, mask-trace DP."""
     rng = random.Random(R * 1000 + W)
-    aligner._h.set_kernel_options(kernel != "mask", kernel == "checkpoint")
+    aligner._h.set_kernel_options(kernel != "mask", kernel == "checkpoint", kernel != "mask")
     aligner.set_tuning(R, W)
     try:
         pairs = []
@@ -211,6 +211,37 @@ def test_geometries_linear_dna(aligner, oracle, R, W, mode, kernel):
         st = aligner.stats()
         if mode != "local":
             assert st["checkpoint"] == (kernel == "checkpoint") and st["tagged"] == (kernel != "mask"), st
+    finally:
+        aligner.set_tuning(0, 0)
+        aligner._h.set_kernel_options(True)
+
+
+@pytest.mark.parametrize("kernel", ["affine_checkpoint", "mask"])
+@pytest.mark.parametrize("R,W", [(2, 1), (2, 16), (4, 3), (4, 8), (8, 2), (8, 5)])
+@pytest.mark.parametrize("mode,a,b", [("local", -11, -1), ("global", -11, -1), ("semiglobal", -3, -1),
+                                      ("overlap", -5, -2), ("fitting", -4, -1), ("local", -2, -2),
+                                      ("global", -1, -2)])
+def test_geometries_affine(aligner, oracle, R, W, mode, a, b, kernel):
+    """The affine / local / protein path at every strip height: score-only DP with per-chunk
+    checkpoints + traceback recomputing full 4-bit-trace chunks, against the mask-trace kernel;
+    DNA and protein, pairs spanning several strips and the LDS mailbox / HBM round wraps."""
+    rng = random.Random(R * 1000 + W + a * 7 + b)
+    aligner._h.set_kernel_options(True, True, kernel == "affine_checkpoint")
+    aligner.set_tuning(R, W)
+    try:
+        for alpha, scoring in ((DNA, "blosum62"), (PROT, "blosum62")):
+            pairs = []
+            for n1, n2 in ((1500, 1400), (700, 2100), (64 * R * 3 + 1, 333), (640, 640), (2, 5),
+                           (2100, 1900), (65, 1), (1, 70)):
+                if mode == "fitting" and n1 < n2:
+                    n1, n2 = n2, n1
+                s1 = rand_seq(rng, n1, alpha)
+                s2 = mutate(rng, s1, alpha, 0.15)[:n2]
+                pairs.append((s1, s2))
+            check_batch(aligner, oracle, mode, pairs, scoring, a, b, fresh=False)
+            st = aligner.stats()
+            if not (a >= b and mode != "local" and alpha == DNA):
+                assert st["checkpoint"] == (kernel == "affine_checkpoint") and st["tagged"] == 0, st
     finally:
         aligner.set_tuning(0, 0)
         aligner._h.set_kernel_options(True)

@@ -57,10 +57,19 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--check", type=int, default=0)
     ap.add_argument("--pipeline", type=int, default=2)
+    ap.add_argument("--R", type=int, default=0)
+    ap.add_argument("--waves", type=int, default=0)
+    ap.add_argument("--kernel-options", type=int, default=7)
+    ap.add_argument("--timing", action="store_true", help="finish-kernel cycle breakdown (stderr)")
     args = ap.parse_args()
+    if args.timing:
+        os.environ["BG_FINISH_TIMING"] = "1"
     from biogarden_amd import _native
     h = _native.Handle(0)
     h.set_pipeline(args.pipeline)
+    h.set_tuning(args.R, args.waves)
+    h.set_kernel_options(bool(args.kernel_options & 1), bool(args.kernel_options & 2),
+                         bool(args.kernel_options & 4))
     sc = _native.builtin_scoring(_native.BG_BLOSUM62)
     for i, name in enumerate(args.configs):
         rng = np.random.default_rng(0xB10A11F0 + int(name[1:]))

@@ -1,7 +1,7 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 1000 python -m pytest tests -x -q -m gpu ${PYTEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/gpu_tests.log 2>&1
 rc=$?
 echo "exit $rc" >> gpurun_out/gpu_tests.log
 tail -40 gpurun_out/gpu_tests.log
