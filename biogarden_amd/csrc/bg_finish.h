@@ -521,83 +521,93 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             continue;
           }
         } else {
-          // Affine gaps: the same pointer jumping over (cell, state) nodes — 3 per lane, node id
-          // state*64 + lane.  An X (Y) node whose x_trace (y_trace) is 'M' falls back to M
-          // without moving (aligner.rs:566-585), so its next pointer is that cell's M node's.
-          const bool jumpable = !(c & (kCodeMiss | kCodeBorder)) && (MODE != BGK_LOCAL || (c & 3) != 3);
-          if (jumpable) {
-            if ((dk | dl) != 0) { reanchor(k, l); }
+          // Affine gaps.  Inside the neighbourhood the X / Y runs of the 3-state walk are resolved
+          // first: an X node at (dk, dl) moves up until the first cell whose x_trace is 'M'
+          // (there it falls back to M without moving, aligner.rs:566-585) or that ends the walk,
+          // found by one find-first-set over a 64-bit lane mask; the same for Y along the row.
+          // What is left is a chain over the 64 M nodes with weights (ops per hop), resolved by
+          // pointer jumping with one ds_bpermute per round; the ops are emitted in parallel.
+          const bool termC = (c & (kCodeMiss | kCodeBorder)) || (MODE == BGK_LOCAL && (c & 3) == 3);
+          if (!termC) {
+            if ((dk | dl) != 0) reanchor(k, l);
             const int cl = codes;
-            const bool term = (cl & (kCodeMiss | kCodeBorder)) || (MODE == BGK_LOCAL && (cl & 3) == 3);
-            const int mvM = (int)(kLutM >> (4 * (cl & 15)) >> 2) & 3;   // 1 diag, 2 up, 3 left
-            const int mvX = (cl & 4) ? mvM : 2;
-            const int mvY = (cl & 8) ? mvM : 3;
-            int P[3], D[3], OP[3], INFO[3];
-#pragma unroll
-            for (int st = 0; st < 3; ++st) {
-              const int mv = st == 0 ? mvM : (st == 1 ? mvX : mvY);
-              const int nk = (lane >> 3) + (mv != 3), nl = (lane & 7) + (mv != 2);
-              const int ns = mv == 2 ? 1 : (mv == 3 ? 2 : 0);      // state after the move
-              const bool ex = !term && (nk >= 8 || nl >= 8);
-              const int self = st * 64 + lane;
-              P[st] = (term || ex) ? self : ns * 64 + nk * 8 + nl;
-              D[st] = (term || ex) ? 0 : 1;
-              OP[st] = mv - 1;
-              INFO[st] = (ex ? 1 : 0) | (mv << 1) | (ns << 3);
-            }
-            // node value lookup: value of node `node` from the lane holding it
-            auto bperm3 = [&](const int (&v)[3], int node) {
-              const int src = (node & 63) * 4;
-              const int r0 = __builtin_amdgcn_ds_bpermute(src, v[0]);
-              const int r1 = __builtin_amdgcn_ds_bpermute(src, v[1]);
-              const int r2 = __builtin_amdgcn_ds_bpermute(src, v[2]);
-              const int sl = node >> 6;
-              return sl == 0 ? r0 : (sl == 1 ? r1 : r2);
+            const bool tm = (cl & (kCodeMiss | kCodeBorder)) || (MODE == BGK_LOCAL && (cl & 3) == 3);
+            const u64 Tm = ballot(tm);
+            const u64 TX = Tm | ballot(cl & 4);        // a run up stops here (x_trace 'M' or end)
+            const u64 TY = Tm | ballot(cl & 8);
+            auto emit = [&](int pos, int n, int op) {  // ops pos .. pos+n-1 of this walk
+              for (int q = 0; q < n; ++q) ob[cap - 1 - (ntail + pos + q)] = (uint8_t)op;
             };
-            int J[4][3];
-#pragma unroll
-            for (int st = 0; st < 3; ++st) J[0][st] = P[st];
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {                        // p <- p(p), d <- d + d(p)
-              int PK[3];
-#pragma unroll
-              for (int st = 0; st < 3; ++st) PK[st] = P[st] | (D[st] << 8);
-#pragma unroll
-              for (int st = 0; st < 3; ++st) {
-                const int qv = bperm3(PK, P[st]);
-                P[st] = qv & 255;
-                D[st] += qv >> 8;
+            // the run the walk is in at the anchor (state X / Y), resolved in scalar
+            int s0 = 0;
+            if (state != 0) {
+              const u64 m = state == 1 ? (TX & 0x0101010101010101ull) : (TY & 0xFFull);
+              int run = 8, endRun = 1;
+              if (m) {
+                s0 = (int)__builtin_ctzll(m);
+                run = state == 1 ? (s0 >> 3) : (s0 & 7);
+                endRun = (int)((Tm >> s0) & 1);
               }
-              if (rr < 3) {
-#pragma unroll
-                for (int st = 0; st < 3; ++st) J[rr + 1][st] = P[st];
+              if (lane == 0) emit(ncore, run, state);
+              ncore += run;
+              if (state == 1) k -= run; else l -= run;
+              if (endRun) continue;                    // an end cell (scalar path) or the edge
+              state = 0;
+            }
+            // per-lane M node: hop target P (self = chain end), hop weight w and op, and for
+            // chain ends the trailing run E, the final cell (fk << 4 | fl) and state
+            const int dkl = lane >> 3, dll = lane & 7, mt = cl & 3;
+            int P = lane, w = 0, op = 0, E = 0, fin = (dkl << 4) | dll, fst = 0;
+            if (!tm) {
+              if (mt == 0) {
+                if (dkl < 7 && dll < 7) { P = lane + 9; w = 1; }
+                else { E = 1; fin = ((dkl + 1) << 4) | (dll + 1); }
+              } else {
+                const bool up = mt == 1;
+                op = up ? 1 : 2;
+                const u64 lineMask = up ? (0x0101010101010101ull << dll) : (0xFFull << (dkl * 8));
+                const u64 m = (up ? TX : TY) & lineMask & ~((2ull << lane) - 1);   // strictly beyond
+                if (!m) {
+                  E = up ? 8 - dkl : 8 - dll;
+                  fin = up ? ((8 << 4) | dll) : ((dkl << 4) | 8);
+                  fst = up ? 1 : 2;
+                } else {
+                  const int bpos = (int)__builtin_ctzll(m);
+                  const int dist = up ? (bpos >> 3) - dkl : (bpos & 7) - dll;
+                  if ((Tm >> bpos) & 1) { E = dist; fin = ((bpos >> 3) << 4) | (bpos & 7); fst = up ? 1 : 2; }
+                  else { P = bpos; w = dist; }
+                }
               }
             }
-            const int entry = state * 64;                           // (anchor cell, state)
-            int x = entry;
+            // pointer jumping: p <- p(p), d <- d + d(p), h <- h + h(p)  (chains <= 14 hops)
+            int PK = P | (w << 8) | ((P != lane ? 1 : 0) << 16);
+            int J[4];
+            J[0] = P;
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr) {
+              const int qv = __builtin_amdgcn_ds_bpermute((PK & 255) * 4, PK);
+              PK = (qv & 255) | ((PK & ~255) + (qv & ~255));
+              if (rr < 3) J[rr + 1] = PK & 255;
+            }
+            const int Dall = (PK >> 8) & 255;                      // weight to the chain's end
+            const int Pn = rdlane(PK & 255, s0), Dn = rdlane(Dall, s0), Hn = rdlane(PK >> 16, s0);
+            // lane m takes the m-th node from s0 and writes its hop's ops
+            int x = s0;
 #pragma unroll
             for (int bb = 0; bb < 4; ++bb) {
-              const int y = bperm3(J[bb], x);
+              const int y = __builtin_amdgcn_ds_bpermute(x * 4, J[bb]);
               x = ((lane >> bb) & 1) ? y : x;
             }
-            const int opx = bperm3(OP, x);
-            const int Pn = rdlane(state == 0 ? P[0] : (state == 1 ? P[1] : P[2]), 0);
-            const int Dn = rdlane(state == 0 ? D[0] : (state == 1 ? D[1] : D[2]), 0);
-            const int sP = Pn >> 6, lP = Pn & 63;
-            const int infoP = rdlane(sP == 0 ? INFO[0] : (sP == 1 ? INFO[1] : INFO[2]), lP);
-            const int exP = infoP & 1, mvP = (infoP >> 1) & 3, nsP = infoP >> 3;
-            const int nops = Dn + exP;
-            if (lane < nops) ob[cap - 1 - (ntail + ncore + lane)] = (uint8_t)opx;
-            ncore += nops;
-            k -= lP >> 3;
-            l -= lP & 7;
-            if (exP) {
-              k -= (mvP != 3);
-              l -= (mvP != 2);
-              state = nsP;
-            } else {
-              state = sP;
-            }
+            const int wx = __builtin_amdgcn_ds_bpermute(x * 4, w | (op << 8));
+            const int dx = __builtin_amdgcn_ds_bpermute(x * 4, Dall);
+            if (lane < Hn) emit(ncore + Dn - dx, wx & 255, wx >> 8);
+            const int En = rdlane(E, Pn), finN = rdlane(fin, Pn), fstN = rdlane(fst, Pn);
+            if (lane == Hn) emit(ncore + Dn, En, fstN);
+            ncore += Dn + En;
+            k = k0 - (finN >> 4);
+            l = l0 - (finN & 15);
+            state = fstN;
+            ++nJump;
             continue;
           }
         }
