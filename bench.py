@@ -25,7 +25,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s
+# int32 VALU: a wave64 instruction occupies its SIMD ~4 cycles (v_max3 / v_add_sdwa / DPP measured
+# 4.4 at 4 waves per SIMD, profiles/r01/micro_valu_rates.txt), i.e. 16 lanes per SIMD per cycle
+VALU_PEAK_OPS = 256 * 4 * 16 * 2.4e9   # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz int32 lane-ops/s
+VALU_CYC_PER_INSTR = 4.4
 SEED = 0xB10A11F0 + 5          # seed = 0xB10A11F0 + config index (metric = 5)
 
 
@@ -62,10 +65,21 @@ def load_pmc(workload):
         return {}
 
 
-# Register-only ceiling of the tagged kernel's step (tools/micro/tag_step.hip on MI355X, 16 waves
-# per CU, profiles/r01/micro_tag_step.txt): the same per-cell VALU sequence with no LDS, HBM,
-# strip pipeline or traceback.  DP cells/s by strip height R.
+# Register-only ceiling of the tagged full-trace kernel's step (tools/micro/tag_step.hip on MI355X,
+# 16 waves per CU, profiles/r01/micro_tag_step.txt): 5R + 2 instructions per 64R cells.
 TAG_REGISTER_CEILING = {4: 6.94e12, 5: 6.60e12, 8: 7.01e12, 10: 6.94e12}
+
+
+def register_ceiling(st):
+    """DP cells/s if every SIMD issued the kernel's step instructions back to back at
+    VALU_CYC_PER_INSTR: score-only linear step 2R + 2 instructions per 64R cells (v_add_sdwa +
+    v_max3 per cell, DPP + profile address per step); tagged full trace from the micro-benchmark."""
+    R = st["R"]
+    if st["tagged"] and st["checkpoint"]:
+        return 256 * 4 * 2.4e9 / VALU_CYC_PER_INSTR * 64 * R / (2 * R + 2), "2R+2 per 64R cells"
+    if st["tagged"] and R in TAG_REGISTER_CEILING:
+        return TAG_REGISTER_CEILING[R], "micro-benchmark (5R+2 per 64R cells)"
+    return None, None
 
 
 def main():
@@ -198,9 +212,9 @@ def main():
         valu.update({"instr_per_cell_measured": round(per_cell, 3),
                      "lane_ops_achieved": per_cell * cells_per_s,
                      "frac_of_lane_peak": round(per_cell * cells_per_s / VALU_PEAK_OPS, 4)})
-    if st["tagged"] and st["R"] in TAG_REGISTER_CEILING:
-        ceil_ = TAG_REGISTER_CEILING[st["R"]]
-        valu.update({"register_ceiling_cells_per_s": ceil_,
+    ceil_, how = register_ceiling(st)
+    if ceil_:
+        valu.update({"register_ceiling_cells_per_s": round(ceil_, -9), "register_ceiling_model": how,
                      "frac_of_register_ceiling": round(cells_per_s / ceil_, 4)})
 
     # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0 only)

@@ -20,7 +20,8 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_align_batch", "bg_batch_prepare", "bg_batch_execute", "bg_batch_fetch",
            "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
            "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
-           "bg_set_pipeline", "bg_set_kernel_options"]
+           "bg_set_pipeline", "bg_set_kernel_options", "bg_edit_distance_batch",
+           "bg_lcs_batch"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -99,6 +100,12 @@ def lib():
                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     L.bg_batch_export.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.POINTER(ctypes.c_size_t)]
+    pair_args = [ctypes.c_void_p, ctypes.c_size_t,
+                 ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                 ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t)]
+    L.bg_edit_distance_batch.argtypes = pair_args + [ctypes.POINTER(ctypes.c_uint64)]
+    L.bg_lcs_batch.argtypes = pair_args + [c_u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_uint64)]
     _LIB = L
     return L
 
@@ -214,6 +221,26 @@ class Handle:
         n = ctypes.c_size_t(nbytes)
         check(lib().bg_batch_export(self._p, ctypes.c_void_p(device_ptr), ctypes.byref(n)))
         return n.value
+
+    def edit_distance_batch(self, pairs):
+        """analysis::seq::edit_distance over pairs [(s1, s2)] -> [int]."""
+        a1, n1, a2, n2, _ = self._arrays(pairs)
+        n = len(pairs)
+        out = (ctypes.c_uint64 * max(n, 1))()
+        check(lib().bg_edit_distance_batch(self._p, n, a1, n1, a2, n2, out))
+        return [int(out[p]) for p in range(n)]
+
+    def lcs_batch(self, pairs):
+        """processing::patterns::longest_common_subsequence over pairs -> [bytes]."""
+        a1, n1, a2, n2, _ = self._arrays(pairs)
+        n = len(pairs)
+        cap = max(1, sum(min(len(x), len(y)) for x, y in pairs))
+        buf = (ctypes.c_uint8 * cap)()
+        off = (ctypes.c_uint64 * max(n, 1))()
+        ln = (ctypes.c_uint64 * max(n, 1))()
+        check(lib().bg_lcs_batch(self._p, n, a1, n1, a2, n2, buf, cap, off, ln))
+        raw = bytes(buf)
+        return [raw[off[p]:off[p] + ln[p]] for p in range(n)]
 
     def stats(self):
         st = BgStats()

@@ -211,6 +211,10 @@ __device__ __forceinline__ void aff_chunk(AffStrip<R, LOCAL>& S, const AffCtx& C
 // trip); the operands arrive through the same one-step-ahead LDS pipeline as the forward pass.
 // FIND (local end cell): the first column j of row `fq` of lane `fl` with M == target is
 // returned in `found` (-1 if none in this chunk).
+// LCS (processing::patterns::longest_common_subsequence, src/processing/patterns.rs:88-98, run as
+// a global alignment with S = +1 / -1 and a = b = 0, whose M is the reference's match table): a
+// match takes the diagonal whatever its ties, so both "not Y" and "not X" are also set where the
+// diagonal candidate reaches M (m - d - 1 < 0; a mismatch's diagonal is always strictly lower).
 template <bool LOCAL>
 __host__ __device__ constexpr int ack_planes() { return LOCAL ? 5 : 4; }
 
@@ -218,7 +222,7 @@ __device__ __forceinline__ unsigned sign_in(unsigned acc, int diff) {
   return __builtin_amdgcn_alignbit(acc, (unsigned)diff, 31);   // (acc << 1) | (diff < 0)
 }
 
-template <int R, bool LOCAL, bool FIRST, bool FIND>
+template <int R, bool LOCAL, bool FIRST, bool FIND, bool LCS = false>
 __device__ __forceinline__ void aff_recomp(AffStrip<R, LOCAL>& S, const AffCtx& C, int c,
                                            uint32_t* slot, int fq, int fl, int target, int& found) {
   const int a = C.a;
@@ -259,8 +263,9 @@ __device__ __forceinline__ void aff_recomp(AffStrip<R, LOCAL>& S, const AffCtx& 
         const int m = imax3(d, x, y);
         // the empty asm pins each shift to its step (else LLVM sinks them all to the flush and
         // keeps every step's differences live)
-        tr[0][k] = sign_in(uu ? tr[0][k] : 0u, y - m);
-        tr[1][k] = sign_in(uu ? tr[1][k] : 0u, x - m);
+        const int dg = LCS ? m - d - 1 : 0;             // < 0: the diagonal reaches M
+        tr[0][k] = sign_in(uu ? tr[0][k] : 0u, (y - m) | dg);
+        tr[1][k] = sign_in(uu ? tr[1][k] : 0u, (x - m) | dg);
         tr[2][k] = sign_in(uu ? tr[2][k] : 0u, mo - xs);
         tr[3][k] = sign_in(uu ? tr[3][k] : 0u, S.M[k] - ys);
         asm volatile("" : "+v"(tr[0][k]), "+v"(tr[1][k]), "+v"(tr[2][k]), "+v"(tr[3][k]));

@@ -113,7 +113,13 @@ struct BgFinishArgs {
   const int32_t* bndX;
   int32_t kdim;
   int32_t area_ints;
-  int32_t flags;           // bit 0: affine walk without pointer jumping (experiments, BG_NO_JUMP)
+  int32_t flags;           // BG_FIN_* below
+};
+
+// BgFinishArgs::flags
+enum {
+  BG_FIN_SCORE_ONLY = 2,   // end cell and score only, no traceback (analysis::seq::edit_distance)
+  BG_FIN_LCS = 4           // LCS tie rule in the recomputed trace; out2 receives the op codes
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

@@ -176,7 +176,7 @@ __device__ void build_prof_aff(const BgFinishArgs& F, const BgPair& P, int s, in
   }
 }
 
-template <int R, bool LOCAL, bool FIND>
+template <int R, bool LOCAL, bool FIND, bool LCS = false>
 __device__ void recompute_chunk_aff(const BgFinishArgs& F, const BgPair& P, int s, int c,
                                     uint32_t* slot, int* area, const int* profTab, int lane,
                                     int fq, int fl, int target, int* foundOut) {
@@ -217,8 +217,8 @@ __device__ void recompute_chunk_aff(const BgFinishArgs& F, const BgPair& P, int 
   C.profLane = reinterpret_cast<const uint8_t*>(profTab + lane * RW);
   C.codeLane = stage + 63 - lane;
   int found = -1;
-  if (c == 0) aff_recomp<R, LOCAL, true, FIND>(S, C, c, slot, fq, fl, target, found);
-  else aff_recomp<R, LOCAL, false, FIND>(S, C, c, slot, fq, fl, target, found);
+  if (c == 0) aff_recomp<R, LOCAL, true, FIND, LCS>(S, C, c, slot, fq, fl, target, found);
+  else aff_recomp<R, LOCAL, false, FIND, LCS>(S, C, c, slot, fq, fl, target, found);
   if constexpr (FIND) {
     if (lane == fl) *foundOut = found;
   }
@@ -666,10 +666,16 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         __syncthreads();
       }
       if (wid < nl) {
-        if constexpr (ACK)
-          recompute_chunk_aff<R, MODE == BGK_LOCAL, false>(F, P, reqS, list[wid], win + (size_t)myz * kSlotDw,
-                                                           ckArea + wid * ckAreaInts, profShared, lane,
-                                                           0, 0, 0, nullptr);
+        if constexpr (ACK) {
+          uint32_t* slotp = win + (size_t)myz * kSlotDw;
+          int* areap = ckArea + wid * ckAreaInts;
+          if (MODE == BGK_GLOBAL && (F.flags & BG_FIN_LCS))
+            recompute_chunk_aff<R, false, false, true>(F, P, reqS, list[wid], slotp, areap, profShared, lane,
+                                                       0, 0, 0, nullptr);
+          else
+            recompute_chunk_aff<R, MODE == BGK_LOCAL, false>(F, P, reqS, list[wid], slotp, areap, profShared,
+                                                             lane, 0, 0, 0, nullptr);
+        }
         else
           recompute_chunk<R>(F, P, reqS, list[wid], win + (size_t)myz * kSlotDw,
                              ckArea + wid * ckAreaInts, lane);
@@ -770,7 +776,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     const uint8_t ch1 = op != 2 ? f.s1[p1++] : (uint8_t)'-';
     const uint8_t ch2 = op != 1 ? f.s2[p2++] : (uint8_t)'-';
     ob[x] = ch1;
-    ob2[x] = ch2;
+    ob2[x] = (F.flags & BG_FIN_LCS) ? (uint8_t)op : ch2;   // LCS: the caller keeps op-0 columns
   }
   if (tid == 0) {
     BgResult res;

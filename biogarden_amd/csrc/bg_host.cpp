@@ -29,6 +29,7 @@ extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes(int win_bytes);
 extern "C" int bg_finish_window_bytes(int R, int affine, size_t npairs, int cus);
 extern "C" void* bg_export_kernel_ptr();
+extern "C" void* bg_global_score_kernel_ptr();
 extern "C" void* bg_dp_aff_kernel_ptr(int R, int local);
 extern "C" int bg_dp_aff_head_bytes(void);
 extern "C" int bg_dp_aff_wave_lds_bytes(int R, int K);
@@ -105,6 +106,7 @@ struct bg_aligner {
   int allowCkpt = 1;
   int allowAck = 1;
   int ckpt = 0;                    // tagged path: score-only DP + checkpoint traceback
+  int finFlags = 0;                // BG_FIN_* for the finish kernel (edit distance, LCS)
   int ack = 0;                     // affine / local path: score-only DP (bg_aff_kernel.hip) +
                                    // traceback over recomputed full-trace chunks
   size_t lds = 0;
@@ -852,13 +854,16 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.bndX = S.bndX.as<int32_t>();
     F.kdim = h->kdim;
     F.area_ints = 0;
-    F.flags = std::getenv("BG_NO_JUMP") ? 1 : 0;
+    F.flags = h->finFlags;
     if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(64 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, h->stream2));
     }
     void* args[] = {&F};
-    if (h->ack) {
+    if (h->finFlags & BG_FIN_SCORE_ONLY) {
+      BG_HIP(hipLaunchKernel(bg_global_score_kernel_ptr(), dim3((np + 255) / 256), dim3(256), args, 0,
+                             h->stream2));
+    } else if (h->ack) {
       int win = 0, area = 0;
       const size_t lds = bg_finish_ack_lds_bytes(h->R, h->kdim, h->local, &win, &area);
       F.win_bytes = win;
@@ -1073,5 +1078,109 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   }
   BG_HIP(hipStreamSynchronize(h->stream));
   *bytes = need;
+  return BG_OK;
+}
+
+// ------------------------------------------------------------------ edit distance, LCS
+// Both run on the aligner's hot path with a byte-equality scoring over the bytes the batch holds
+// (at most 32 distinct, else BG_E_ALPHABET):
+//   analysis::seq::edit_distance (src/analysis/seq.rs:105-130) = -(global score) with S = 0 / -1
+//     and a = b = -1 (the Levenshtein recurrence is the linear-gap global DP), score only;
+//   processing::patterns::longest_common_subsequence (src/processing/patterns.rs:82-118) = the
+//     diagonal columns of the global traceback with S = +1 / -1, a = b = 0 (M is the match
+//     table), under the LCS tie rule (BG_FIN_LCS), on the score-only kernel family that
+//     recomputes full-trace chunks.
+static int equality_scoring(size_t npairs, const uint8_t* const* s1, const size_t* n1,
+                            const uint8_t* const* s2, const size_t* n2, int32_t match,
+                            int32_t mismatch, bg_scoring* sc) {
+  bool seen[256] = {false};
+  for (size_t p = 0; p < npairs; ++p) {
+    if ((n1[p] && !s1[p]) || (n2[p] && !s2[p])) return BG_E_ARG;
+    for (size_t i = 0; i < n1[p]; ++i) seen[s1[p][i]] = true;
+    for (size_t j = 0; j < n2[p]; ++j) seen[s2[p][j]] = true;
+  }
+  std::memset(sc, 0, sizeof(*sc));
+  std::memset(sc->code, 0xFF, sizeof(sc->code));
+  int k = 0;
+  for (int x = 0; x < 256; ++x)
+    if (seen[x]) {
+      if (k == 32) return BG_E_ALPHABET;
+      sc->code[x] = (uint8_t)k++;
+    }
+  sc->alphabet_size = std::max(k, 1);
+  for (int r = 0; r < 32; ++r)
+    for (int c = 0; c < 32; ++c) sc->table[r * 32 + c] = r == c ? match : mismatch;
+  return BG_OK;
+}
+
+// results of the last execute in caller order (no strings)
+static int fetch_scores(bg_aligner* h, std::vector<BgResult>& out) {
+  int rc = bg_synchronize(h);
+  if (rc) return rc;
+  const size_t np = h->plan.size();
+  h->hres.resize(np);
+  if (np)
+    BG_HIP(hipMemcpy(h->hres.data(), h->slot[h->lastSlot].results.p, sizeof(BgResult) * np,
+                     hipMemcpyDeviceToHost));
+  out.assign(h->npairs, BgResult{});
+  for (size_t q = 0; q < np; ++q) out[h->order_[q]] = h->hres[q];
+  return BG_OK;
+}
+
+extern "C" int bg_edit_distance_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s1,
+                                      const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                                      uint64_t* dist) {
+  if (!h || (npairs && (!s1 || !n1 || !s2 || !n2 || !dist))) return BG_E_ARG;
+  bg_scoring sc;
+  int rc = equality_scoring(npairs, s1, n1, s2, n2, 0, -1, &sc);
+  if (rc) return rc;
+  h->finFlags = BG_FIN_SCORE_ONLY;
+  rc = bg_batch_prepare(h, BG_GLOBAL, npairs, s1, n1, s2, n2, &sc, -1, -1);
+  if (!rc) rc = bg_batch_execute(h);
+  std::vector<BgResult> res;
+  if (!rc) rc = fetch_scores(h, res);
+  h->finFlags = 0;
+  h->prepared = false;       // the flags belong to this call's batch
+  if (rc) return rc;
+  for (size_t p = 0; p < npairs; ++p) {
+    if (h->prestatus[p] >= 0) return BG_E_ARG;        // unreachable: equality scores every byte
+    dist[p] = (uint64_t)(-(int64_t)res[p].score);
+  }
+  return BG_OK;
+}
+
+extern "C" int bg_lcs_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s1,
+                            const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                            uint8_t* out, size_t out_cap, uint64_t* offset, uint64_t* len) {
+  if (!h || (npairs && (!s1 || !n1 || !s2 || !n2 || !offset || !len))) return BG_E_ARG;
+  size_t need = 0;
+  for (size_t p = 0; p < npairs; ++p) need += std::min(n1[p], n2[p]);
+  if (need && (!out || out_cap < need)) return BG_E_ARG;
+  bg_scoring sc;
+  int rc = equality_scoring(npairs, s1, n1, s2, n2, 1, -1, &sc);
+  if (rc) return rc;
+  const int allowTag = h->allowTag, allowAck = h->allowAck;
+  h->allowTag = 0;           // the LCS tie rule lives in the recomputing affine-family traceback
+  h->allowAck = 1;
+  h->finFlags = BG_FIN_LCS;
+  rc = bg_batch_prepare(h, BG_GLOBAL, npairs, s1, n1, s2, n2, &sc, 0, 0);
+  if (!rc && !h->ack) rc = BG_E_SCORE_RANGE;          // sizes beyond the frame's range
+  if (!rc) rc = bg_batch_execute(h);
+  std::vector<bg_pair_result> res(npairs);
+  std::vector<uint8_t> a1(h->outBytes + 1), ops(h->outBytes + 1);
+  if (!rc) rc = bg_batch_fetch(h, res.data(), a1.data(), ops.data(), h->outBytes + 1);
+  h->allowTag = allowTag;
+  h->allowAck = allowAck;
+  h->finFlags = 0;
+  h->prepared = false;
+  if (rc) return rc;
+  size_t o = 0;
+  for (size_t p = 0; p < npairs; ++p) {
+    offset[p] = o;
+    const size_t base = res[p].offset;
+    for (uint32_t x = 0; x < res[p].len; ++x)
+      if (ops[base + x] == 0) out[o++] = a1[base + x];       // diagonal column = a match
+    len[p] = o - offset[p];
+  }
   return BG_OK;
 }

@@ -366,6 +366,25 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
 
 #include "bg_finish.h"
 
+// ------------------------------------------------------------------ score only (global)
+// End cell of global mode without a traceback (aligner.rs:112: M(n1, n2); borders :98-104), for
+// the score-only callers (analysis::seq::edit_distance): one thread per pair.
+__global__ __launch_bounds__(256) void bg_global_score_kernel(BgFinishArgs F) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= F.npairs) return;
+  const BgPair& P = F.pairs[q];
+  int score;
+  if (P.n1 == 0) score = row0_M(BGK_GLOBAL, P.n2, F.open, F.ext);
+  else if (P.n2 == 0) score = col0_M(BGK_GLOBAL, P.n1, F.open, F.ext);
+  else score = F.aux[P.aux_off + P.n1];                // lastcol[n1] = M(n1, n2)
+  BgResult res;
+  res.status = 0; res.score = score; res.end_i = P.n1; res.end_j = P.n2;
+  res.out_start = (uint32_t)(P.n1 + P.n2); res.out_len = 0;
+  res.start1 = (uint32_t)P.n1; res.start2 = (uint32_t)P.n2;
+  F.results[P.index] = res;
+}
+extern "C" void* bg_global_score_kernel_ptr() { return (void*)&bg_global_score_kernel; }
+
 // ------------------------------------------------------------------ export (for collectives)
 
 __global__ __launch_bounds__(256) void bg_export_kernel(BgExportArgs E) {

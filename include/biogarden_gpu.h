@@ -166,6 +166,23 @@ int bg_set_pipeline(bg_aligner* h, int depth);
  * than four symbols (else the mask-trace kernel).  Takes effect at the next bg_batch_prepare. */
 int bg_set_kernel_options(bg_aligner* h, int allow_tagged);
 
+/* analysis::seq::edit_distance (src/analysis/seq.rs:105-130) for a batch of pairs: unit-cost
+ * Levenshtein distance over raw bytes, dist[p] = the reference's Ok(usize).  Runs the global DP
+ * (byte equality 0 / -1, open = extend = -1) score-only on the GPU.  BG_E_ALPHABET when the
+ * batch holds more than 32 distinct byte values.  Replaces the prepared batch. */
+int bg_edit_distance_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s1,
+                           const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                           uint64_t* dist);
+
+/* processing::patterns::longest_common_subsequence (src/processing/patterns.rs:82-118) for a
+ * batch: the reference's subsequence (its tie rules) of pair p is out[offset[p] .. +len[p]);
+ * out_cap >= sum of min(n1, n2).  Global DP (byte equality +1 / -1, open = extend = 0) with the
+ * LCS tie rule in the traceback.  BG_E_ALPHABET beyond 32 distinct bytes.  Replaces the
+ * prepared batch.  shortest_common_supersequence (:198-235) is the host-side merge around it. */
+int bg_lcs_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s1, const size_t* n1,
+                 const uint8_t* const* s2, const size_t* n2, uint8_t* out, size_t out_cap,
+                 uint64_t* offset, uint64_t* len);
+
 const char* bg_status_string(int status);
 int bg_abi_version(void);
 

@@ -439,3 +439,58 @@ double or_align_batch(int mode, size_t npairs, const uint8_t* const* s1, const s
   free(th);
   return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ---------------------------------------------------------------------------------------------
+ * analysis::seq::edit_distance (src/analysis/seq.rs:105-130): the unit-cost Levenshtein table
+ * over raw bytes, memo[i][0] = i, memo[0][j] = j, memo[i][j] = min(memo[i-1][j-1] + (s1[i-1] !=
+ * s2[j-1]), min(memo[i][j-1] + 1, memo[i-1][j] + 1)).  The reference's u128 cells never exceed
+ * max(n1, n2), so uint64 is exact.  Two rows instead of the full table (same values). */
+uint64_t or_edit_distance(const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2) {
+  uint64_t* prev = (uint64_t*)malloc((n2 + 1) * sizeof(uint64_t));
+  uint64_t* cur = (uint64_t*)malloc((n2 + 1) * sizeof(uint64_t));
+  for (size_t j = 0; j <= n2; ++j) prev[j] = j;                    /* :113-115 */
+  for (size_t i = 1; i <= n1; ++i) {                               /* :118-127 */
+    cur[0] = i;                                                    /* :110-112 */
+    for (size_t j = 1; j <= n2; ++j) {
+      const uint64_t d = prev[j - 1] + (s1[i - 1] != s2[j - 1]);
+      const uint64_t l = cur[j - 1] + 1, u = prev[j] + 1;
+      const uint64_t m = l < u ? l : u;
+      cur[j] = d < m ? d : m;
+    }
+    uint64_t* t = prev; prev = cur; cur = t;
+  }
+  const uint64_t r = prev[n2];
+  free(prev); free(cur);
+  return r;
+}
+
+/* processing::patterns::longest_common_subsequence (src/processing/patterns.rs:82-118): the
+ * match table with its tie rules (a match always takes the diagonal; otherwise up only when
+ * strictly greater than left, :88-98) and the walk from (n1, n2) while the cell is non-zero,
+ * pushing seq1[i-1] on diagonal moves (:104-114).  Writes the subsequence to out (capacity
+ * >= min(n1, n2)); returns its length. */
+size_t or_lcs(const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2, uint8_t* out) {
+  const size_t W = n2 + 1;
+  uint32_t* L = (uint32_t*)calloc((n1 + 1) * W, sizeof(uint32_t));
+  uint8_t* prev = (uint8_t*)calloc((n1 + 1) * W, 1);    /* 0 diag, 1 up, 2 left */
+  for (size_t i = 1; i <= n1; ++i)
+    for (size_t j = 1; j <= n2; ++j) {
+      if (s1[i - 1] == s2[j - 1]) {
+        L[i * W + j] = L[(i - 1) * W + j - 1] + 1; prev[i * W + j] = 0;
+      } else if (L[(i - 1) * W + j] > L[i * W + j - 1]) {
+        L[i * W + j] = L[(i - 1) * W + j]; prev[i * W + j] = 1;
+      } else {
+        L[i * W + j] = L[i * W + j - 1]; prev[i * W + j] = 2;
+      }
+    }
+  size_t i = n1, j = n2, len = 0;
+  while (L[i * W + j] != 0) {
+    const uint8_t p = prev[i * W + j];
+    if (p == 0) { out[len++] = s1[i - 1]; --i; --j; }
+    else if (p == 1) --i;
+    else --j;
+  }
+  for (size_t x = 0; x < len / 2; ++x) { const uint8_t t = out[x]; out[x] = out[len - 1 - x]; out[len - 1 - x] = t; }
+  free(L); free(prev);
+  return len;
+}

@@ -70,6 +70,12 @@ double or_align_batch(int mode, size_t npairs, const uint8_t* const* s1, const s
                       const uint8_t* const* s2, const size_t* n2, const or_scoring* sc, int32_t a,
                       int32_t b, int nthreads, int exact, int32_t* scores, int* statuses);
 
+/* analysis::seq::edit_distance (src/analysis/seq.rs:105-130) */
+uint64_t or_edit_distance(const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2);
+/* processing::patterns::longest_common_subsequence (src/processing/patterns.rs:82-118);
+ * out capacity >= min(n1, n2); returns the subsequence length */
+size_t or_lcs(const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2, uint8_t* out);
+
 #ifdef __cplusplus
 }
 #endif

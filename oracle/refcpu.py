@@ -54,6 +54,12 @@ def lib():
                                      ctypes.POINTER(ctypes.c_int32),
                                      ctypes.POINTER(ctypes.c_int)]
         L.or_align_batch.restype = ctypes.c_double
+        L.or_edit_distance.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                       ctypes.c_size_t]
+        L.or_edit_distance.restype = ctypes.c_uint64
+        L.or_lcs.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t,
+                             ctypes.c_char_p]
+        L.or_lcs.restype = ctypes.c_size_t
         _LIB = L
     return _LIB
 
@@ -122,3 +128,38 @@ def align_batch(mode, pairs, score="blosum62", a=-11, b=-1, nthreads=1, exact=Tr
     secs = lib().or_align_batch(MODES[mode], n, s1, n1, s2, n2, ctypes.byref(sc), a, b,
                                 nthreads, 1 if exact else 0, scores, sts)
     return secs, list(scores), list(sts)
+
+
+def edit_distance(s1, s2):
+    """analysis::seq::edit_distance (src/analysis/seq.rs:105-130)."""
+    s1, s2 = bytes(s1), bytes(s2)
+    return int(lib().or_edit_distance(s1, len(s1), s2, len(s2)))
+
+
+def longest_common_subsequence(s1, s2):
+    """processing::patterns::longest_common_subsequence (src/processing/patterns.rs:82-118)."""
+    s1, s2 = bytes(s1), bytes(s2)
+    out = ctypes.create_string_buffer(min(len(s1), len(s2)) + 1)
+    n = lib().or_lcs(s1, len(s1), s2, len(s2), out)
+    return out.raw[:n]
+
+
+def shortest_common_supersequence(s1, s2):
+    """processing::patterns::shortest_common_supersequence (src/processing/patterns.rs:198-235):
+    interleave both sequences around their LCS."""
+    lcs = longest_common_subsequence(s1, s2)
+    it1, it2 = iter(bytes(s1)), iter(bytes(s2))
+    out = bytearray()
+    for c in lcs:
+        for x in it1:
+            if x == c:
+                break
+            out.append(x)
+        for x in it2:
+            if x == c:
+                break
+            out.append(x)
+        out.append(c)
+    out.extend(it1)
+    out.extend(it2)
+    return bytes(out)

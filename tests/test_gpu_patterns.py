@@ -1,0 +1,94 @@
+"""GPU parity of the §8(f) widening rows that run on the alignment DP:
+analysis::seq::edit_distance (src/analysis/seq.rs:105-130) and
+processing::patterns::{longest_common_subsequence, shortest_common_supersequence}
+(src/processing/patterns.rs:82-118, 198-235), through bg_edit_distance_batch / bg_lcs_batch.
+Bit-exact against the oracle (oracle/refcpu.c), itself pinned by the reference's goldens
+(tests/integration.rs:69-74, 135-149) and doctests.
+"""
+import os
+import random
+
+import pytest
+
+from conftest import REF_FIX, read_fasta
+
+pytestmark = pytest.mark.gpu
+
+DNA = b"ACGT"
+PROT = b"ACDEFGHIKLMNPQRSTVWY"
+
+
+def rand_seq(rng, n, alpha):
+    return bytes(rng.choice(alpha) for _ in range(n))
+
+
+def mutate(rng, s, alpha, rate=0.2):
+    out = bytearray()
+    for ch in s:
+        r = rng.random()
+        if r < rate / 3:
+            continue
+        if r < 2 * rate / 3:
+            out.append(rng.choice(alpha))
+        out.append(rng.choice(alpha) if rng.random() < rate / 3 else ch)
+    return bytes(out)
+
+
+def test_reference_goldens():
+    from biogarden_amd.analysis.seq import edit_distance
+    from biogarden_amd.ds.sequence import Sequence
+    from biogarden_amd.processing.patterns import (longest_common_subsequence,
+                                                   shortest_common_supersequence)
+    inp = read_fasta(os.path.join(REF_FIX, "input", "edit_distance.fasta"))
+    assert edit_distance(Sequence(inp[0][1]), Sequence(inp[1][1])) == 299          # integration.rs:73
+    assert edit_distance(Sequence("ACTGGATTC"), Sequence("ACGT")) == 5              # seq.rs:97-104
+    inp = read_fasta(os.path.join(REF_FIX, "input", "longest_common_subseq.fasta"))
+    out = read_fasta(os.path.join(REF_FIX, "output", "longest_common_subseq.fasta"))
+    assert longest_common_subsequence(Sequence(inp[0][1]), Sequence(inp[1][1])) == Sequence(out[0][1])
+    assert longest_common_subsequence(Sequence("AACCTTGG"), Sequence("ACACTGTGA")) == Sequence("ACCTGG")
+    inp = read_fasta(os.path.join(REF_FIX, "input", "shortest_common_superseq.fasta"))
+    out = read_fasta(os.path.join(REF_FIX, "output", "shortest_common_superseq.fasta"))
+    assert shortest_common_supersequence(Sequence(inp[0][1]), Sequence(inp[1][1])) == Sequence(out[0][1])
+    assert shortest_common_supersequence(Sequence("TGCATA"), Sequence("ATCTGAT")) == Sequence("ATGCATGAT")
+
+
+@pytest.mark.parametrize("alpha", [DNA, PROT, b"AC", b"abcdefghijklmnopqrstuvwxyz0123-."])
+def test_random_vs_oracle(oracle, alpha):
+    from biogarden_amd.analysis.seq import edit_distance_batch
+    from biogarden_amd.processing.patterns import (longest_common_subsequence_batch,
+                                                   shortest_common_supersequence_batch)
+    rng = random.Random(len(alpha))
+    lens = [0, 1, 2, 5, 63, 64, 65, 130, 257, 600, 1100, 2300]
+    pairs = []
+    for _ in range(40):
+        n1, n2 = rng.choice(lens), rng.choice(lens)
+        s1 = rand_seq(rng, n1, alpha)
+        s2 = mutate(rng, s1, alpha)[:n2] if rng.random() < 0.6 else rand_seq(rng, n2, alpha)
+        pairs.append((s1, s2))
+    got = edit_distance_batch(pairs)
+    assert got == [oracle.edit_distance(a, b) for a, b in pairs]
+    lcs = longest_common_subsequence_batch(pairs)
+    assert [bytes(x.chain) for x in lcs] == [oracle.longest_common_subsequence(a, b) for a, b in pairs]
+    scs = shortest_common_supersequence_batch(pairs)
+    assert [bytes(x.chain) for x in scs] == [oracle.shortest_common_supersequence(a, b) for a, b in pairs]
+
+
+def test_long_pairs(oracle):
+    """Pairs spanning many strips and chunks (the recomputing traceback crosses strips)."""
+    from biogarden_amd.analysis.seq import edit_distance_batch
+    from biogarden_amd.processing.patterns import longest_common_subsequence_batch
+    rng = random.Random(11)
+    pairs = []
+    for n1, n2 in ((5000, 4700), (3000, 6100), (4096, 4096)):
+        s1 = rand_seq(rng, n1, DNA)
+        pairs.append((s1, mutate(rng, s1, DNA, 0.3)[:n2]))
+    assert edit_distance_batch(pairs) == [oracle.edit_distance(a, b) for a, b in pairs]
+    assert [bytes(x.chain) for x in longest_common_subsequence_batch(pairs)] == \
+        [oracle.longest_common_subsequence(a, b) for a, b in pairs]
+
+
+def test_alphabet_limit():
+    from biogarden_amd import _native
+    from biogarden_amd.analysis.seq import edit_distance
+    with pytest.raises(RuntimeError, match="32"):
+        edit_distance(bytes(range(40)), bytes(range(40, 80)))

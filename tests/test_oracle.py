@@ -81,3 +81,44 @@ def test_blosum62_dna_block():
             "GT": -2}
     for k, v in want.items():
         assert b[ix[k[0]]][ix[k[1]]] == v == b[ix[k[1]]][ix[k[0]]]
+
+
+# ------------------------------------------------------------------ edit distance / LCS / SCS
+# tests/integration.rs:69-74 (299), :135-149 (fixtures) and the doctests seq.rs:97-104,
+# patterns.rs:73-80, 190-196
+
+def test_edit_distance_golden(oracle):
+    inp = read_fasta(os.path.join(REF_FIX, "input", "edit_distance.fasta"))
+    assert oracle.edit_distance(inp[0][1], inp[1][1]) == 299
+    assert oracle.edit_distance(b"ACTGGATTC", b"ACGT") == 5
+
+
+def test_lcs_scs_goldens(oracle):
+    inp = read_fasta(os.path.join(REF_FIX, "input", "longest_common_subseq.fasta"))
+    out = read_fasta(os.path.join(REF_FIX, "output", "longest_common_subseq.fasta"))
+    assert oracle.longest_common_subsequence(inp[0][1], inp[1][1]) == out[0][1]
+    inp = read_fasta(os.path.join(REF_FIX, "input", "shortest_common_superseq.fasta"))
+    out = read_fasta(os.path.join(REF_FIX, "output", "shortest_common_superseq.fasta"))
+    assert oracle.shortest_common_supersequence(inp[0][1], inp[1][1]) == out[0][1]
+    assert oracle.longest_common_subsequence(b"AACCTTGG", b"ACACTGTGA") == b"ACCTGG"
+    assert oracle.shortest_common_supersequence(b"TGCATA", b"ATCTGAT") == b"ATGCATGAT"
+
+
+def test_edit_distance_small_cases(oracle):
+    assert oracle.edit_distance(b"", b"") == 0
+    assert oracle.edit_distance(b"", b"ACG") == 3
+    assert oracle.edit_distance(b"ACGT", b"") == 4
+    assert oracle.edit_distance(b"kitten", b"sitting") == 3
+
+
+def test_scs_merge_matches_oracle(oracle):
+    """The product's host-side supersequence merge (patterns.rs:198-235) around the oracle's LCS."""
+    import random
+
+    from biogarden_amd.processing.patterns import _merge
+    rng = random.Random(5)
+    for _ in range(200):
+        a = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(0, 40)))
+        b = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(0, 40)))
+        lcs = oracle.longest_common_subsequence(a, b)
+        assert _merge(a, b, lcs) == oracle.shortest_common_supersequence(a, b)
