@@ -387,4 +387,70 @@ class SequenceAligner {
 };
 
 }  // namespace alignment
+
+// ------------------------------------------------------------------ the DP's other callers
+// The reference's free functions that are alignment DPs, on the same GPU kernels.  They take an
+// explicit device handle (a SequenceAligner-owned bg_aligner would do as well); one call = one
+// GPU batch.
+namespace detail {
+struct PairArrays {            // one pair as the C ABI's pointer / length arrays
+  const uint8_t* p1[1];
+  const uint8_t* p2[1];
+  size_t n1[1], n2[1];
+  PairArrays(const ds::Sequence& a, const ds::Sequence& b)
+      : p1{a.chain.data()}, p2{b.chain.data()}, n1{a.chain.size()}, n2{b.chain.size()} {}
+};
+class Device {
+ public:
+  static bg_aligner* get() {
+    static Device d;
+    if (!d.h_) throw DeviceError(BG_E_HIP);
+    return d.h_;
+  }
+ private:
+  Device() : h_(bg_aligner_new(0)) {}
+  ~Device() { if (h_) bg_aligner_free(h_); }
+  bg_aligner* h_;
+};
+}  // namespace detail
+
+namespace analysis {
+namespace seq {
+// analysis::seq::edit_distance (src/analysis/seq.rs:105-130)
+inline Result<size_t> edit_distance(const ds::Sequence& seq1, const ds::Sequence& seq2) {
+  detail::PairArrays a(seq1, seq2);
+  uint64_t d = 0;
+  check(bg_edit_distance_batch(detail::Device::get(), 1, a.p1, a.n1, a.p2, a.n2, &d));
+  return Result<size_t>((size_t)d);
+}
+}  // namespace seq
+}  // namespace analysis
+
+namespace processing {
+namespace patterns {
+// processing::patterns::longest_common_subsequence (src/processing/patterns.rs:82-118)
+inline ds::Sequence longest_common_subsequence(const ds::Sequence& seq1, const ds::Sequence& seq2) {
+  detail::PairArrays a(seq1, seq2);
+  std::vector<uint8_t> out(std::min(seq1.len(), seq2.len()) + 1);
+  uint64_t off = 0, len = 0;
+  check(bg_lcs_batch(detail::Device::get(), 1, a.p1, a.n1, a.p2, a.n2, out.data(), out.size(), &off, &len));
+  return ds::Sequence(std::vector<uint8_t>(out.begin() + off, out.begin() + off + len));
+}
+// processing::patterns::shortest_common_supersequence (:198-235): both sequences interleaved
+// around their LCS, residues differing from the next LCS residue first
+inline ds::Sequence shortest_common_supersequence(const ds::Sequence& seq1, const ds::Sequence& seq2) {
+  const ds::Sequence lcs = longest_common_subsequence(seq1, seq2);
+  std::vector<uint8_t> out;
+  size_t i = 0, j = 0;
+  for (uint8_t c : lcs.chain) {
+    while (i < seq1.len()) { const uint8_t x = seq1.chain[i++]; if (x == c) break; out.push_back(x); }
+    while (j < seq2.len()) { const uint8_t x = seq2.chain[j++]; if (x == c) break; out.push_back(x); }
+    out.push_back(c);
+  }
+  out.insert(out.end(), seq1.chain.begin() + i, seq1.chain.end());
+  out.insert(out.end(), seq2.chain.begin() + j, seq2.chain.end());
+  return ds::Sequence(std::move(out));
+}
+}  // namespace patterns
+}  // namespace processing
 }  // namespace biogarden

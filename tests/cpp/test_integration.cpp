@@ -44,6 +44,21 @@ int main(int argc, char** argv) {
   try { aligner.global_alignment(ds::Sequence("ACgT"), ds::Sequence("ACG"), score::blosum62, -1, -1); }
   catch (const ReferencePanic&) { panicked = true; }
   fails += !panicked;
+  // tests/integration.rs:69-74 and :135-149 (edit distance, LCS, SCS)
+  {
+    auto ed = io::fasta::read_tile(fix + "/input/edit_distance.fasta");
+    const size_t d = analysis::seq::edit_distance(ed[0], ed[1]).unwrap();
+    std::printf("edit_distance %zu (expect 299)\n", d);
+    fails += d != 299;
+    auto li = io::fasta::read_tile(fix + "/input/longest_common_subseq.fasta");
+    auto lo = io::fasta::read_tile(fix + "/output/longest_common_subseq.fasta");
+    const bool lok = processing::patterns::longest_common_subsequence(li[0], li[1]) == lo[0];
+    auto si = io::fasta::read_tile(fix + "/input/shortest_common_superseq.fasta");
+    auto so = io::fasta::read_tile(fix + "/output/shortest_common_superseq.fasta");
+    const bool sok = processing::patterns::shortest_common_supersequence(si[0], si[1]) == so[0];
+    std::printf("lcs %s scs %s\n", lok ? "ok" : "MISMATCH", sok ? "ok" : "MISMATCH");
+    fails += !lok + !sok;
+  }
   std::printf("%s\n", fails ? "FAILED" : "integration ok");
   return fails ? 1 : 0;
 }
