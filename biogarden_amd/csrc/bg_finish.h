@@ -484,21 +484,18 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             const bool ex = !term && (nk >= 8 || nl >= 8);          // the move leaves the block
             int p = (term || ex) ? lane : nk * 8 + nl;
             int d = (term || ex) ? 0 : 1;
-            int J[4];
-            J[0] = p;
-#pragma unroll
-            for (int rr = 0; rr < 4; ++rr) {                        // p <- p(p), d <- d + d(p)
-              const int qv = __builtin_amdgcn_ds_bpermute(p * 4, p | (d << 8));
-              p = qv & 255;
-              d += qv >> 8;
-              if (rr < 3) J[rr + 1] = p;
-            }
-            // lane m finds the m-th cell of the chain from the anchor, then its move
+            // p <- p(p), d <- d + d(p) (4 rounds: chains of up to 16 cells), interleaved with
+            // lane m finding the m-th cell of the chain from the anchor: round rr of that search
+            // needs the pointers after 2^rr hops, i.e. p before jumping round rr, so the two
+            // ds_bpermute chains overlap
             int x = 0;
 #pragma unroll
-            for (int bb = 0; bb < 4; ++bb) {
-              const int y = __builtin_amdgcn_ds_bpermute(x * 4, J[bb]);
-              x = ((lane >> bb) & 1) ? y : x;
+            for (int rr = 0; rr < 4; ++rr) {
+              const int y = __builtin_amdgcn_ds_bpermute(x * 4, p);
+              const int qv = __builtin_amdgcn_ds_bpermute(p * 4, p | (d << 8));
+              x = ((lane >> rr) & 1) ? y : x;
+              p = qv & 255;
+              d += qv >> 8;
             }
             const int opx = __builtin_amdgcn_ds_bpermute(x * 4, mv - 1);
             const int Pn = rdlane(p, 0), Dn = rdlane(d, 0);
@@ -581,23 +578,18 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             }
             // pointer jumping: p <- p(p), d <- d + d(p), h <- h + h(p)  (chains <= 14 hops)
             int PK = P | (w << 8) | ((P != lane ? 1 : 0) << 16);
-            int J[4];
-            J[0] = P;
+            // interleaved with lane m finding the m-th node from s0 (see the linear jumper)
+            int x = s0;
 #pragma unroll
             for (int rr = 0; rr < 4; ++rr) {
+              const int y = __builtin_amdgcn_ds_bpermute(x * 4, PK & 255);
               const int qv = __builtin_amdgcn_ds_bpermute((PK & 255) * 4, PK);
+              x = ((lane >> rr) & 1) ? y : x;
               PK = (qv & 255) | ((PK & ~255) + (qv & ~255));
-              if (rr < 3) J[rr + 1] = PK & 255;
             }
             const int Dall = (PK >> 8) & 255;                      // weight to the chain's end
             const int Pn = rdlane(PK & 255, s0), Dn = rdlane(Dall, s0), Hn = rdlane(PK >> 16, s0);
-            // lane m takes the m-th node from s0 and writes its hop's ops
-            int x = s0;
-#pragma unroll
-            for (int bb = 0; bb < 4; ++bb) {
-              const int y = __builtin_amdgcn_ds_bpermute(x * 4, J[bb]);
-              x = ((lane >> bb) & 1) ? y : x;
-            }
+            // lane m (the m-th node from s0) writes its hop's ops
             const int wx = __builtin_amdgcn_ds_bpermute(x * 4, w | (op << 8));
             const int dx = __builtin_amdgcn_ds_bpermute(x * 4, Dall);
             if (lane < Hn) emit(ncore + Dn - dx, wx & 255, wx >> 8);
