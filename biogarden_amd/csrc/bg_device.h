@@ -114,6 +114,7 @@ struct BgFinishArgs {
   int32_t kdim;
   int32_t area_ints;
   int32_t flags;           // BG_FIN_* below
+  int32_t nslots;          // checkpoint modes: recomputed-chunk slots in use (0: all)
 };
 
 // BgFinishArgs::flags

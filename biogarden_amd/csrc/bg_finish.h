@@ -245,7 +245,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   if constexpr (ACK) ckArea += F.area_ints;
   int profS = -1;                                     // ACK: strip whose profile is built
   constexpr int kSlotDw = ACK ? ack_slot_dw<R, MODE == BGK_LOCAL>() : ck_slot_dw<R>();
-  int* jscr = ckArea + (CK ? 4 * ckAreaInts : 0);
+  const int NWV = (int)(blockDim.x >> 6);              // waves: walker + recompute helpers
+  int* jscr = ckArea + (CK ? NWV * ckAreaInts : 0);
   // checkpoint mode: direct-mapped table (strip & 31, chunk & 31) -> (s << 20 | c << 4 | slot)
   unsigned* ckMap = reinterpret_cast<unsigned*>(jscr);
   if (CK) {
@@ -373,6 +374,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   }();
   constexpr int kCkSlots = ACK ? ack_slots<R>() : ck_slots<R>();
   int ckS[kCkSlots], ckC[kCkSlots];                  // checkpoint mode: resident chunks
+  // slots in use (the host trades cache for more resident workgroups on many-pair batches)
+  const int nSlots = (F.nslots > 0 && F.nslots < kCkSlots) ? F.nslots : kCkSlots;
   int ckNext = 0;                                    // next slot to fill (FIFO)
 #pragma unroll
   for (int z = 0; z < kCkSlots; ++z) { ckS[z] = -1; ckC[z] = -1; }
@@ -643,7 +646,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       // recompute the requested chunk and up to three chunks to its left (the walk heads up and
       // left), one per wave, into the oldest slots
       int list[4], nl = 0;
-      for (int d = 0; d < 4; ++d) {
+      for (int d = 0; d < NWV && d < 4; ++d) {
         const int cc = reqB0 - d;
         if (cc < 0) break;
         bool res = false;
@@ -651,7 +654,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         for (int z = 0; z < kCkSlots; ++z) res |= (ckS[z] == reqS && ckC[z] == cc);
         if (!res || d == 0) list[nl++] = cc;
       }
-      const int myz = (ckNext + wid) % kCkSlots;
+      const int myz = (ckNext + wid) % nSlots;
       if (ACK && reqS != profS) {                    // the recomputing waves share the profile
         build_prof_aff<R>(F, P, reqS, profShared, tid, NT);
         profS = reqS;
@@ -673,7 +676,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                              ckArea + wid * ckAreaInts, lane);
       }
       for (int x = 0; x < nl; ++x) {
-        const int z = (ckNext + x) % kCkSlots;
+        const int z = (ckNext + x) % nSlots;
         int oldS = -1, oldC = -1;
 #pragma unroll
         for (int zz = 0; zz < kCkSlots; ++zz)
@@ -687,7 +690,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
               ((unsigned)reqS << 20) | ((unsigned)list[x] << 4) | (unsigned)z;
         }
       }
-      ckNext = (ckNext + nl) % kCkSlots;
+      ckNext = (ckNext + nl) % nSlots;
       k0 = -1000000;
     } else {
       const int nb = (stripBlocks - reqB0) < NBW ? (stripBlocks - reqB0) : NBW;

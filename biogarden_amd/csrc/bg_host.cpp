@@ -23,7 +23,7 @@ extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
 extern "C" int bg_dp_has_R(int R, int affine, int local, int dna);
 extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt);
 extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode);
-extern "C" size_t bg_finish_ck_lds_bytes(int R, int* win_bytes);
+extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
 extern "C" int bg_dp_tag_wave_lds_bytes(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes(int win_bytes);
@@ -34,7 +34,8 @@ extern "C" void* bg_dp_aff_kernel_ptr(int R, int local);
 extern "C" int bg_dp_aff_head_bytes(void);
 extern "C" int bg_dp_aff_wave_lds_bytes(int R, int K);
 extern "C" void* bg_finish_ack_kernel_ptr(int R, int mode);
-extern "C" size_t bg_finish_ack_lds_bytes(int R, int K, int local, int* win_bytes, int* area_ints);
+extern "C" size_t bg_finish_ack_lds_bytes(int R, int K, int local, int nslots, int nw, int* win_bytes,
+                                          int* area_ints);
 
 #include "bg_tables.inc"
 
@@ -339,11 +340,26 @@ static void* fin_fn(const bg_aligner* h, int R) {
   if (h->ckpt) return bg_finish_ck_kernel_ptr(R, h->mode);
   return bg_finish_kernel_ptr(R, h->affine, h->mode);
 }
+// Finish workgroup of the checkpoint modes: waves (the walker + recompute helpers) and
+// recomputed-chunk slots.  Few pairs: 4 waves and every slot (the walk's latency is the step's
+// tail).  Many pairs: fewer waves and slots, so more pairs walk per CU at once (the walks are
+// latency-bound, one wave each).  BG_FIN_WAVES / BG_FIN_SLOTS override (experiments).
+static void fin_geom(const bg_aligner* h, size_t np, int* nw, int* nslots) {
+  *nw = 4;
+  *nslots = 0;
+  if ((h->ack || h->ckpt) && np > (size_t)h->cus * 2) { *nw = 1; *nslots = 2; }
+  if (const char* e = std::getenv("BG_FIN_WAVES")) *nw = std::min(4, std::max(1, std::atoi(e)));
+  if (const char* e = std::getenv("BG_FIN_SLOTS")) *nslots = std::max(0, std::atoi(e));
+  if (*nslots && *nslots < *nw + 1) *nslots = *nw + 1;
+}
+
 // LDS of one finish workgroup (and the window / recompute-area sizes it launches with)
 static size_t fin_lds(const bg_aligner* h, int R, size_t np, int* win, int* area) {
   *area = 0;
-  if (h->ack) return bg_finish_ack_lds_bytes(R, h->kdim, h->local, win, area);
-  if (h->ckpt) return bg_finish_ck_lds_bytes(R, win);
+  int nw = 4, ns = 0;
+  fin_geom(h, np, &nw, &ns);
+  if (h->ack) return bg_finish_ack_lds_bytes(R, h->kdim, h->local, ns, nw, win, area);
+  if (h->ckpt) return bg_finish_ck_lds_bytes(R, ns, nw, win);
   *win = bg_finish_window_bytes(R, h->affine, np, h->cus);
   return bg_finish_lds_bytes(*win);
 }
@@ -860,26 +876,29 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, h->stream2));
     }
     void* args[] = {&F};
+    int fnw = 4, fns = 0;
+    fin_geom(h, np, &fnw, &fns);
+    F.nslots = fns;
     if (h->finFlags & BG_FIN_SCORE_ONLY) {
       BG_HIP(hipLaunchKernel(bg_global_score_kernel_ptr(), dim3((np + 255) / 256), dim3(256), args, 0,
                              h->stream2));
     } else if (h->ack) {
       int win = 0, area = 0;
-      const size_t lds = bg_finish_ack_lds_bytes(h->R, h->kdim, h->local, &win, &area);
+      const size_t lds = bg_finish_ack_lds_bytes(h->R, h->kdim, h->local, fns, fnw, &win, &area);
       F.win_bytes = win;
       F.area_ints = area;
       F.tag = 2;
       F.affine = 1;
       void* ffn = bg_finish_ack_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(256), args, lds, h->stream2));
+      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, h->stream2));
     } else if (h->ckpt) {
       int win = 0;
-      const size_t lds = bg_finish_ck_lds_bytes(h->R, &win);
+      const size_t lds = bg_finish_ck_lds_bytes(h->R, fns, fnw, &win);
       F.win_bytes = win;
       void* ffn = bg_finish_ck_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(256), args, lds, h->stream2));
+      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, h->stream2));
     } else {
       F.win_bytes = bg_finish_window_bytes(h->R, h->affine, np, h->cus);
       BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(h->R, h->affine, h->mode), dim3(np), dim3(256), args,

@@ -487,19 +487,21 @@ extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode) {
     default: return nullptr;
   }
 }
-// LDS of the checkpoint finish kernel: chunk slots (the scan aliases them), scalars, 4 recompute areas
-extern "C" size_t bg_finish_ck_lds_bytes(int R, int* win_bytes) {
-  int slot = 0, area = 0, nslot = 8;
+// LDS of the checkpoint finish kernel with `nslots` chunk slots (0: the maximum) and `nw` waves:
+// chunk slots (the scan aliases them), scalars, nw recompute areas, the chunk map
+extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes) {
+  int slot = 0, area = 0, maxs = 8;
   switch (R) {
-    case 2: slot = ck_slot_dw<2>(); area = ck_wave_ints<2>(); nslot = ck_slots<2>(); break;
-    case 3: slot = ck_slot_dw<3>(); area = ck_wave_ints<3>(); nslot = ck_slots<3>(); break;
-    case 4: slot = ck_slot_dw<4>(); area = ck_wave_ints<4>(); nslot = ck_slots<4>(); break;
-    case 5: slot = ck_slot_dw<5>(); area = ck_wave_ints<5>(); nslot = ck_slots<5>(); break;
-    case 8: slot = ck_slot_dw<8>(); area = ck_wave_ints<8>(); nslot = ck_slots<8>(); break;
-    default: slot = ck_slot_dw<10>(); area = ck_wave_ints<10>(); nslot = ck_slots<10>(); break;
+    case 2: slot = ck_slot_dw<2>(); area = ck_wave_ints<2>(); maxs = ck_slots<2>(); break;
+    case 3: slot = ck_slot_dw<3>(); area = ck_wave_ints<3>(); maxs = ck_slots<3>(); break;
+    case 4: slot = ck_slot_dw<4>(); area = ck_wave_ints<4>(); maxs = ck_slots<4>(); break;
+    case 5: slot = ck_slot_dw<5>(); area = ck_wave_ints<5>(); maxs = ck_slots<5>(); break;
+    case 8: slot = ck_slot_dw<8>(); area = ck_wave_ints<8>(); maxs = ck_slots<8>(); break;
+    default: slot = ck_slot_dw<10>(); area = ck_wave_ints<10>(); maxs = ck_slots<10>(); break;
   }
-  *win_bytes = nslot * slot * 4;
-  return (size_t)*win_bytes + 64 * 4 + 4 * (size_t)area * 4 + kCkMapEntries * 4;  // + chunk map
+  const int ns = (nslots > 0 && nslots < maxs) ? nslots : maxs;
+  *win_bytes = std::max(ns * slot * 4, 2 * 256 * 4);
+  return (size_t)*win_bytes + 64 * 4 + (size_t)nw * area * 4 + kCkMapEntries * 4;  // + chunk map
 }
 
 template <int R, bool AF>
