@@ -120,7 +120,8 @@ struct BgFinishArgs {
 // BgFinishArgs::flags
 enum {
   BG_FIN_SCORE_ONLY = 2,   // end cell and score only, no traceback (analysis::seq::edit_distance)
-  BG_FIN_LCS = 4           // LCS tie rule in the recomputed trace; out2 receives the op codes
+  BG_FIN_LCS = 4,          // LCS tie rule in the recomputed trace; out2 receives the op codes
+  BG_FIN_SYNC = 8          // linear checkpoint traceback: recompute at barriers (BG_FIN_SYNC=1, A/B)
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

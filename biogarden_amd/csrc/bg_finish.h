@@ -240,6 +240,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   // chunk held by slot z (-1: empty); per-wave recompute areas follow the scan
   int* ckArea = sh + 64;
   constexpr bool ACK = CK && AFFINE;                  // affine / local checkpoint traceback
+  constexpr bool LIN_CK = CK && !AFFINE;              // linear checkpoint traceback
   const int ckAreaInts = ACK ? kAckWaveInts : ck_wave_ints<R>();
   int* profShared = ckArea;                           // ACK: the strip's profile entries
   if constexpr (ACK) ckArea += F.area_ints;
@@ -388,7 +389,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     const int t = ll + r, bl = t >> 5;
     if constexpr (CK) {
       const int cc = t >> 6;
-      const unsigned e = ckMap[ck_map_idx(sidx, cc)];   // (s << 20 | c << 4 | slot)
+      // (s << 20 | c << 4 | slot); an atomic load: helper waves publish chunks concurrently
+      const unsigned e = __hip_atomic_load(&ckMap[ck_map_idx(sidx, cc)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if ((e >> 4) != (((unsigned)sidx << 16) | (unsigned)cc) || e == 0xFFFFFFFFu) return kCodeMiss;
       const int z = (int)(e & 15);
       if constexpr (ACK) {
@@ -427,8 +429,13 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   };
   // decodes the 8x8 neighbourhood anchored at (k, l): lane (dk, dl) holds cell (k - dk, l - dl)
   u64 tDec = 0, nDec = 0;                                // BG_FINISH_TIMING: decodes
+  bool asyncPos = false;                                 // set below: post the walker's position
   auto reanchor = [&](int ka, int la) {
     k0 = ka; l0 = la;
+    if (asyncPos && lane == 0) {
+      __hip_atomic_store(&sh[34], ka, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_store(&sh[35], la, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     const u64 td0 = F.dbg ? __builtin_readcyclecounter() : 0;
     codes = decode_cell(k0 - (lane >> 3), l0 - (lane & 7));
     if (F.dbg) {
@@ -461,6 +468,102 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   }
   u64 tJump = 0, tMiss = 0, nJump = 0, nMiss = 0;        // BG_FINISH_TIMING instrumentation
   const u64 tWalk0 = __builtin_readcyclecounter();
+
+  // ---- linear checkpoint traceback, asynchronous recomputation.  The helper waves recompute
+  // chunks ahead of the walker instead of all waves meeting at a barrier on every miss: the
+  // walker posts its position (sh[34], sh[35]) and, on a miss, the chunk it needs (sh[33]); a
+  // helper claims a slot under an LDS lock (sh[36]; per slot: chunk key sh[40+z], filling flag
+  // sh[48+z]), recomputes the chunk and publishes it in ckMap; the walker spins on ckMap.  With
+  // no request pending the helpers prefetch the chunks the walk heads into: left in its strip
+  // down to the predicted exit, then the predicted entry of the strip above.  Eviction: a chunk
+  // right of or below the walker is dead (the walk only moves up / left); a request may also
+  // evict any slot outside the walker's 2 x 2 chunk footprint (it is waiting, so it reads none).
+  const bool async = LIN_CK && NWV >= 2 && nSlots >= 5 && !(F.flags & BG_FIN_SYNC);
+  asyncPos = async;
+  if (async) {
+    if (tid == 0) {
+      sh[32] = 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0;
+      for (int z = 0; z < 8; ++z) { sh[40 + z] = -1; sh[48 + z] = 0; }
+    }
+    __syncthreads();
+  }
+  if (async && wid != 0) {
+    const int NCp = P.nc, NSp = P.nstrips;
+    auto enc = [](int key, int z) { return (unsigned)((key >> 16) << 20) | (unsigned)((key & 0xffff) << 4) | (unsigned)z; };
+    auto resident = [&](int key) {
+      const unsigned e = __hip_atomic_load(&ckMap[ck_map_idx(key >> 16, key & 0xffff)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return e != 0xFFFFFFFFu && (int)(e >> 4) == key;
+    };
+    for (;;) {
+      if (__hip_atomic_load(&sh[32], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      int key = -1, zz = -1;
+      if (lane == 0) {
+        while (__hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+          __builtin_amdgcn_s_sleep(1);
+        const int req = __hip_atomic_load(&sh[33], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int kw = __hip_atomic_load(&sh[34], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int lw = __hip_atomic_load(&sh[35], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int vw = kw > 0 ? kw - 1 : 0;
+        const int sw = vw / ROWS, remw = vw - sw * ROWS, ccw = (lw + remw / R) >> 6;
+        const int xA = (lw + 63) >> 6;                     // the strip above, next to the walker
+        const int cExit = (lw - remw) >> 6;                // this strip's chunk at its top row
+        const int xE = (lw - remw + 62) >> 6;              // the strip above's entry chunk
+        auto mk = [&](int ss, int cc) { return (ss < 0 || ss >= NSp || cc < 0 || cc >= NCp) ? -1 : (ss << 16) | cc; };
+        int cand[6];
+        cand[0] = req;
+        cand[1] = mk(sw, ccw);
+        cand[2] = ccw - 1 >= cExit ? mk(sw, ccw - 1) : -1;
+        cand[3] = ccw - 2 >= cExit ? mk(sw, ccw - 2) : -1;
+        cand[4] = mk(sw - 1, xE);
+        cand[5] = mk(sw - 1, xE - 1);
+        auto dead = [&](int kk) { const int ss = kk >> 16, cc = kk & 0xffff; return ss > sw || (ss == sw && cc > ccw); };
+        auto guarded = [&](int kk) {
+          const int ss = kk >> 16, cc = kk & 0xffff;
+          return (ss == sw && (cc == ccw || cc == ccw - 1)) || (ss == sw - 1 && (cc == xA || cc == xA - 1));
+        };
+        for (int q = 0; q < 6 && key < 0; ++q) {
+          const int kk = cand[q];
+          if (kk < 0 || resident(kk)) continue;
+          bool flying = false;
+          for (int z = 0; z < nSlots; ++z) flying |= (sh[48 + z] != 0 && sh[40 + z] == kk);
+          if (flying) continue;
+          // a slot: empty, stale (its chunk no longer in the map), dead, or (request) unguarded
+          int pick = -1;
+          for (int z = 0; z < nSlots && pick < 0; ++z) {
+            if (sh[48 + z]) continue;
+            const int oz = sh[40 + z];
+            const bool stale = oz < 0 || ckMap[ck_map_idx(oz >> 16, oz & 0xffff)] != enc(oz, z);
+            if (stale || dead(oz)) pick = z;
+          }
+          if (pick < 0 && q == 0)
+            for (int z = 0; z < nSlots && pick < 0; ++z)
+              if (!sh[48 + z] && !guarded(sh[40 + z])) pick = z;
+          if (pick < 0) continue;
+          const int oz = sh[40 + pick];
+          if (oz >= 0) {
+            unsigned& oe = ckMap[ck_map_idx(oz >> 16, oz & 0xffff)];
+            if (oe == enc(oz, pick)) __hip_atomic_store(&oe, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          sh[40 + pick] = kk;
+          sh[48 + pick] = 1;
+          key = kk;
+          zz = pick;
+        }
+        __hip_atomic_store(&sh[36], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      key = uni(__shfl(key, 0, 64));
+      zz = uni(__shfl(zz, 0, 64));
+      if (key < 0) { __builtin_amdgcn_s_sleep(8); continue; }
+      recompute_chunk<R>(F, P, key >> 16, key & 0xffff, win + (size_t)zz * kSlotDw,
+                         ckArea + wid * ckAreaInts, lane);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) {
+        __hip_atomic_store(&ckMap[ck_map_idx(key >> 16, key & 0xffff)], enc(key, zz), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_store(&sh[48 + zz], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+  }
   for (;;) {
     int reqS = -1, reqB0 = 0, done = 0;
     if (wid == 0) {
@@ -611,6 +714,29 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           reqS = vr / ROWS;
           const int bl = (l + (vr - reqS * ROWS) / R) >> 5;
           reqB0 = CK ? (bl >> 1) : (bl - NBW + 1 > 0 ? bl - NBW + 1 : 0);
+          if (async) {
+            // post the position and the request, then wait for a helper to publish the chunk
+            const u64 tw0 = F.dbg ? __builtin_readcyclecounter() : 0;
+            const int key = (reqS << 16) | reqB0;
+            if (lane == 0) {
+              __hip_atomic_store(&sh[34], k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_store(&sh[35], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              __hip_atomic_store(&sh[33], key, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            const unsigned* me = &ckMap[ck_map_idx(reqS, reqB0)];
+            int it = 0;
+            for (;; ++it) {
+              const unsigned e = __hip_atomic_load(me, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+              if (e != 0xFFFFFFFFu && (int)(e >> 4) == key) break;
+              if (it > (1 << 22)) break;                   // no helper answered: give up loudly
+              __builtin_amdgcn_s_sleep(1);
+            }
+            if (it > (1 << 22)) { status = 5; done = 1; break; }
+            k0 = -1000000;                                 // decode the neighbourhood again
+            ++nMiss;
+            if (F.dbg) tMiss += __builtin_readcyclecounter() - tw0;
+            continue;
+          }
           break;
         }
         const bool interior = !(c & kCodeBorder);
@@ -634,6 +760,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       }
       __builtin_amdgcn_s_setprio(0);
       if (lane == 0) { sh[4] = reqS; sh[5] = reqB0; sh[6] = done; }
+      if (async && lane == 0) __hip_atomic_store(&sh[32], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
     done = sh[6];

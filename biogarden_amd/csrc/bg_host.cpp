@@ -871,6 +871,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.kdim = h->kdim;
     F.area_ints = 0;
     F.flags = h->finFlags;
+    if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;
     if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(64 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, h->stream2));
