@@ -12,7 +12,7 @@ LIB_PATH = os.path.join(_HERE, "libbiogarden_gpu.so")
 BG_GLOBAL, BG_LOCAL, BG_FITTING, BG_OVERLAP, BG_SEMIGLOBAL = range(5)
 MODES = {"global": BG_GLOBAL, "local": BG_LOCAL, "fitting": BG_FITTING,
          "overlap": BG_OVERLAP, "semiglobal": BG_SEMIGLOBAL}
-BG_OK, BG_INVALID_ARGUMENT_RANGE, BG_INVALID_INPUT_SIZE, BG_UNSCORABLE, BG_REF_DIVERGENT = range(5)
+BG_OK, BG_INVALID_ARGUMENT_RANGE, BG_INVALID_INPUT_SIZE, BG_UNSCORABLE, BG_REF_DIVERGENT, BG_INTERNAL = range(6)
 BG_BLOSUM62, BG_PAM250, BG_UNIT = range(3)
 
 # every symbol include/biogarden_gpu.h declares (checked by tests/test_abi.py)

@@ -165,6 +165,7 @@ extern "C" const char* bg_status_string(int s) {
     case BG_INVALID_INPUT_SIZE: return "InvalidInputSize";
     case BG_UNSCORABLE: return "unscorable byte (reference panics)";
     case BG_REF_DIVERGENT: return "reference would panic/hang (exact-size result returned)";
+    case BG_INTERNAL: return "internal error (traceback recomputation timed out)";
     case BG_E_ARG: return "bad argument";
     case BG_E_HIP: return "HIP error";
     case BG_E_NOMEM: return "out of memory";

@@ -47,8 +47,10 @@ enum {
   BG_INVALID_ARGUMENT_RANGE = 1, /* Err(BioError::InvalidArgumentRange): a > 0 || b > 0 (global/local/fitting) */
   BG_INVALID_INPUT_SIZE = 2,     /* Err(BioError::InvalidInputSize): fitting with len1 < len2 */
   BG_UNSCORABLE = 3,             /* the reference panics in the score closure (byte outside its table) */
-  BG_REF_DIVERGENT = 4           /* the reference (fresh SequenceAligner) panics or hangs on this input;
+  BG_REF_DIVERGENT = 4,          /* the reference (fresh SequenceAligner) panics or hangs on this input;
                                     the result of the exactly-sized DP is returned and flagged */
+  BG_INTERNAL = 5                /* the traceback's walker waited too long for a recomputed chunk (a
+                                    build defect, never expected); the pair's strings are incomplete */
 };
 
 /* Call-level errors (negative return values). */
