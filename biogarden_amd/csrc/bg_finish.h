@@ -731,7 +731,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
               if (it > (1 << 22)) break;                   // no helper answered: give up loudly
               __builtin_amdgcn_s_sleep(1);
             }
-            if (it > (1 << 22)) { status = 5; done = 1; break;   // BG_INTERNAL }
+            if (it > (1 << 22)) { status = 5; done = 1; break; }   // 5: BG_INTERNAL
             k0 = -1000000;                                 // decode the neighbourhood again
             ++nMiss;
             if (F.dbg) tMiss += __builtin_readcyclecounter() - tw0;
