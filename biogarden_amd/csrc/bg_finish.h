@@ -151,6 +151,13 @@ template <int R>
 __host__ __device__ constexpr int ack_prof_ints(int K) { return K * 64 * AffW<R>::v; }
 // chunk map: direct-mapped (strip & 15, chunk & 15) -> (s << 20 | c << 4 | slot)
 constexpr int kCkMapEntries = 256;
+// asynchronous recomputation: prefetch the strip above once the walker is this close to it
+constexpr int kAboveRows = 128;
+// ... and this many chunks ahead of the walker in its strip / in the strip above
+#ifndef BG_SPEC_DEPTH
+#define BG_SPEC_DEPTH 2
+#endif
+constexpr int kSpecDepth = BG_SPEC_DEPTH;
 __device__ __forceinline__ int ck_map_idx(int s, int c) { return ((s & 15) << 4) | (c & 15); }
 
 // this wave-lane's profile entries for strip s, built by the whole workgroup
@@ -466,7 +473,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       if (status) { k = 0; l = 0; }
     }
   }
-  u64 tJump = 0, tMiss = 0, nJump = 0, nMiss = 0;        // BG_FINISH_TIMING instrumentation
+  u64 tJump = 0, tMiss = 0, nJump = 0, nMiss = 0, nRec = 0;   // BG_FINISH_TIMING instrumentation
   const u64 tWalk0 = __builtin_readcyclecounter();
 
   // ---- linear checkpoint traceback, asynchronous recomputation.  The helper waves recompute
@@ -482,7 +489,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   asyncPos = async;
   if (async) {
     if (tid == 0) {
-      sh[32] = 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0;
+      sh[32] = 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0; sh[37] = 0; sh[56] = -1;
       for (int z = 0; z < 8; ++z) { sh[40 + z] = -1; sh[48 + z] = 0; }
     }
     __syncthreads();
@@ -506,22 +513,30 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         const int vw = kw > 0 ? kw - 1 : 0;
         const int sw = vw / ROWS, remw = vw - sw * ROWS, ccw = (lw + remw / R) >> 6;
         const int xA = (lw + 63) >> 6;                     // the strip above, next to the walker
-        const int cExit = (lw - remw) >> 6;                // this strip's chunk at its top row
-        const int xE = (lw - remw + 62) >> 6;              // the strip above's entry chunk
+        // the column where the walk leaves this strip, from its slope since it entered it
+        // (sh[56..58] = strip, row, column of the entry; diagonal until 16 rows are walked)
+        if (sh[56] != sw) { sh[56] = sw; sh[57] = kw; sh[58] = lw; }
+        const int dkIn = sh[57] - kw, dlIn = sh[58] - lw;
+        const int lOut = lw - (dkIn >= 16 ? (int)((long)remw * dlIn / dkIn) : remw);
+        const int cExit = lOut >> 6;                       // this strip's chunk at its top row
+        const int xE = (lOut + 62) >> 6;                   // the strip above's entry chunk
         auto mk = [&](int ss, int cc) { return (ss < 0 || ss >= NSp || cc < 0 || cc >= NCp) ? -1 : (ss << 16) | cc; };
-        int cand[6];
+        int cand[2 + 2 * kSpecDepth];
+        constexpr int NCAND = 2 + 2 * kSpecDepth;
         cand[0] = req;
         cand[1] = mk(sw, ccw);
-        cand[2] = ccw - 1 >= cExit ? mk(sw, ccw - 1) : -1;
-        cand[3] = ccw - 2 >= cExit ? mk(sw, ccw - 2) : -1;
-        cand[4] = mk(sw - 1, xE);
-        cand[5] = mk(sw - 1, xE - 1);
+        // up to kSpecDepth chunks left of the walker in its strip, down to the predicted exit;
+        // the strip above only near its boundary (earlier, the entry column is a poor guess)
+        for (int d = 1; d <= kSpecDepth; ++d) {
+          cand[1 + d] = ccw - d >= cExit ? mk(sw, ccw - d) : -1;
+          cand[1 + kSpecDepth + d] = remw < kAboveRows ? mk(sw - 1, xE + 1 - d) : -1;
+        }
         auto dead = [&](int kk) { const int ss = kk >> 16, cc = kk & 0xffff; return ss > sw || (ss == sw && cc > ccw); };
         auto guarded = [&](int kk) {
           const int ss = kk >> 16, cc = kk & 0xffff;
           return (ss == sw && (cc == ccw || cc == ccw - 1)) || (ss == sw - 1 && (cc == xA || cc == xA - 1));
         };
-        for (int q = 0; q < 6 && key < 0; ++q) {
+        for (int q = 0; q < NCAND && key < 0; ++q) {
           const int kk = cand[q];
           if (kk < 0 || resident(kk)) continue;
           bool flying = false;
@@ -556,6 +571,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       if (key < 0) { __builtin_amdgcn_s_sleep(8); continue; }
       recompute_chunk<R>(F, P, key >> 16, key & 0xffff, win + (size_t)zz * kSlotDw,
                          ckArea + wid * ckAreaInts, lane);
+      if (F.dbg && lane == 0) __hip_atomic_fetch_add(&sh[37], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) {
         __hip_atomic_store(&ckMap[ck_map_idx(key >> 16, key & 0xffff)], enc(key, zz), __ATOMIC_RELEASE,
@@ -818,6 +834,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         }
       }
       ckNext = (ckNext + nl) % nSlots;
+      nRec += nl;
       k0 = -1000000;
     } else {
       const int nb = (stripBlocks - reqB0) < NBW ? (stripBlocks - reqB0) : NBW;
@@ -848,6 +865,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     u64* d = F.dbg + (size_t)P.index * 8;
     d[0] = __builtin_readcyclecounter() - tWalk0;
     d[1] = tJump + tDec; d[2] = nJump + nDec; d[3] = tMiss; d[4] = nMiss; d[5] = (u64)ncore;
+    d[6] = async ? (u64)sh[37] : nRec;
   }
 
   // ---------------- semiglobal prefix gaps (:416-428); every wave knows k, l through sh

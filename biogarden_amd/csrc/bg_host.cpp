@@ -944,11 +944,11 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.p && np) {
     std::vector<unsigned long long> d(8 * np);
     BG_HIP(hipMemcpy(d.data(), h->dbgBuf.p, 64 * np, hipMemcpyDeviceToHost));
-    double s[6] = {0, 0, 0, 0, 0, 0};
+    double s[7] = {0, 0, 0, 0, 0, 0, 0};
     for (size_t p = 0; p < np; ++p)
-      for (int x = 0; x < 6; ++x) s[x] += (double)d[8 * p + x];
-    std::fprintf(stderr, "finish timing (per pair avg, cycles): walk %.0f  jump %.0f (n %.1f)  miss %.0f (n %.1f)  ops %.0f\n",
-                 s[0] / np, s[1] / np, s[2] / np, s[3] / np, s[4] / np, s[5] / np);
+      for (int x = 0; x < 7; ++x) s[x] += (double)d[8 * p + x];
+    std::fprintf(stderr, "finish timing (per pair avg, cycles): walk %.0f  jump %.0f (n %.1f)  miss %.0f (n %.1f)  ops %.0f  chunks recomputed %.1f\n",
+                 s[0] / np, s[1] / np, s[2] / np, s[3] / np, s[4] / np, s[5] / np, s[6] / np);
   }
   h->hres.resize(np);
   uint64_t ob = 0;
