@@ -365,6 +365,15 @@ static size_t fin_lds(const bg_aligner* h, int R, size_t np, int* win, int* area
   return bg_finish_lds_bytes(*win);
 }
 
+// affine / local checkpoint traceback: per-row cost R^2 coefficient.  Fitted on the step, not on
+// the finish kernel alone (C5 at R = 4 / R = 2: finish 1.22x at the same wave count, but the
+// step pays the R = 4 recomputation again as interference with the next DP): 24 picks R = 2 for
+// C5 (tools/c5_sweep.sh, tools/cfg_lib_ab.sh) and keeps C2's R = 2.
+#ifndef BG_FIN_R2
+#define BG_FIN_R2 24.0
+#endif
+static constexpr double kFinR2 = BG_FIN_R2;
+
 static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncomp, int* Rout,
                           int* Wout) {
   const int cand[] = {2, 3, 4, 5, 8, 10};
@@ -390,10 +399,15 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
     const int opsPerStep = h->ack ? (h->local ? 8 * Rc + 4 : 6 * Rc + 4)
                          : h->ckpt ? 2 * Rc + 2 : (h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12));
     const int S = maxn1 ? (int)((maxn1 + 64 * Rc - 1) / (64 * Rc)) : 1;
-    const int wmax = (!h->ack && (h->affine || h->local)) ? 8 : 16;
+    // many pairs on the affine / local checkpoint path: at most 4 waves per pair (C5: R = 2 runs
+    // W = 4 at 2 232 GCUPS, W = 8 at 2 077; every CU holds several pairs anyway)
+    const int wmax = (!h->ack && (h->affine || h->local)) ? 8 : ((h->ack && np >= (size_t)h->cus) ? 4 : 16);
     for (int Wc = 1; Wc <= wmax; ++Wc) {
       if (h->tuneW && Wc != h->tuneW) continue;
       if (Wc > S && !h->tuneW) continue;
+      // many pairs on the affine / local path: wave counts that divide over the 4 SIMDs (W = 3
+      // estimates best for C5 and measures worst: 2 089 GCUPS against 2 232 at R = 2 / W = 4)
+      if (h->ack && np >= (size_t)h->cus && !h->tuneW && (Wc & (Wc - 1))) continue;
       const int wps = (Wc + 3) / 4;                      // waves per SIMD per workgroup
       const int want = (int)((np + h->cus - 1) / h->cus);
       int wg = std::min(want, 32 / Wc);
@@ -452,7 +466,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
         // flight per CU as the finish workgroup's LDS allows
         const double fwg = std::max(1.0, std::floor(160.0 * 1024 / (double)std::max<size_t>(finLds, 1)));
         const double frounds = std::ceil((double)np / ((double)h->cus * fwg));
-        T += frounds * (600.0 + 8.0 * Rc * Rc) * (double)(maxn1 + maxn2) * 0.5;
+        T += frounds * (600.0 + kFinR2 * Rc * Rc) * (double)(maxn1 + maxn2) * 0.5;
       }
       const int wpsAll = wps * wg;
       cands.push_back({T, Rc, Wc, wpsAll, rowc ? 1 : 0});
@@ -463,8 +477,17 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   // pipeline tail the model charges for is filled by the overlapped traceback), then more waves
   // per SIMD, then the estimate
   const Cand* pick = nullptr;
+  if (std::getenv("BG_PLAN_DEBUG"))
+    for (const Cand& c : cands)
+      std::fprintf(stderr, "plan R %d W %d wps %d T %.4g\n", c.R, c.W, c.wps, c.T);
+  // (the affine / local checkpoint path pays taller strips again in the traceback's
+  // recomputation: lowest estimate)
   for (const Cand& c : cands) {
     if (c.T > best * 1.05) continue;
+    if (h->ack) {
+      if (!pick || c.T < pick->T) pick = &c;
+      continue;
+    }
     if (!pick || c.R > pick->R || (c.R == pick->R && (c.wps > pick->wps || (c.wps == pick->wps && c.T < pick->T))))
       pick = &c;
   }
