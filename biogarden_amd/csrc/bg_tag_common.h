@@ -30,6 +30,7 @@ struct TagCtx {
   int* mail;                // LDS mailbox slot for the block finished in this chunk (consumer
                             // in this workgroup), or nullptr: the block goes to HBM
   const uint8_t* profLane;  // LDS: this lane's profile entries (+ scaled code = entry address)
+  int top0, topStep;        // score_chunk<..., TOP0>: M'(0, t0) and its step along row 0
 };
 
 // profile dwords per lane and code: R int8 bytes, padded to an aligned ds_read width
@@ -174,13 +175,16 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 // (v_add_u32_sdwa, v_max3).  No trace: the traceback recomputes the chunks its path crosses
 // from the per-chunk checkpoints with tag_chunk<KIND_RECOMP>.  Every strip's boundary row goes
 // to HBM (the recomputation's top input), plus the LDS mailbox for a consumer in the workgroup.
-template <int R, int VAR, bool WIDE>
+// TOP0 (strip 0, interior chunks): the row above is row 0, M'(0, j) = top0 + (j - t0) topStep
+// (aligner.rs:98-104 borders, linear in j for j >= 1), kept in a scalar register instead of one
+// broadcast LDS read per step — the read that makes single-strip batches (C4) LDS-bound.
+template <int R, int VAR, bool WIDE, bool TOP0 = false>
 __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int c) {
   const int a = C.a;
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
   constexpr int RW = ProfW<R>::v;
-  int nTop = C.bIn[0];
+  int nTop = TOP0 ? C.top0 : C.bIn[0];
   ProfV<RW> nP = load_prof<RW>(C.profLane + C.codeLane[0]);
   int nCode = C.codeLane[1];
   const uint16_t* cl = C.codeLane + 2;
@@ -195,8 +199,10 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
       const ProfV<RW> P = nP;
       nP = load_prof<RW>(C.profLane + nCode);
       nCode = cl[uu];
-      nTop = bi[uu];
+      if constexpr (!TOP0) nTop = bi[uu];
       const int topX = dpp_shr1(topIn, S.Xlast);             // M'(row above, j)
+      // lane 0 keeps the DPP's old operand, the only lane whose row-0 input matters
+      if constexpr (TOP0) nTop = topX + C.topStep;
       int dIn = S.topPrev;                                    // M'(row above, j-1)
       int xo = topX;
 #pragma unroll

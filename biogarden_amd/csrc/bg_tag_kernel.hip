@@ -250,7 +250,14 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         ck[R * BG_WAVE] = S.topPrev;
         if (edge) score_chunk<R, TV_EDGE, WIDE>(S, C, c);
         else if (lastStrip && selRow) score_chunk<R, TV_SEL, WIDE>(S, C, c);
-        else score_chunk<R, TV_FAST, WIDE>(S, C, c);
+        else if (R <= 4 && s == 0) {
+          // row 0 above: M'(0, j) for j >= 1 is linear (semiglobal / local / overlap: M = 0;
+          // global / fitting: a + (j - 1) b)
+          const bool flat = mode == BGK_SEMIGLOBAL || mode == BGK_LOCAL || mode == BGK_OVERLAP;
+          C.topStep = flat ? -a : b - a;
+          C.top0 = wadd(row0_M(mode, c * BG_CHUNK, a, b), -wmul(a, c * BG_CHUNK));
+          score_chunk<R, TV_FAST, WIDE, true>(S, C, c);
+        } else score_chunk<R, TV_FAST, WIDE>(S, C, c);
       } else {
         if (edge) tag_chunk<R, TV_EDGE, WIDE>(S, C, c);
         else if (lastStrip && selRow) tag_chunk<R, TV_SEL, WIDE>(S, C, c);
