@@ -184,22 +184,36 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
   constexpr int RW = ProfW<R>::v;
+  // operand pipeline depth: the profile entries and row-above inputs of the next PF steps are in
+  // flight while a step computes.  One step hides the LDS latency at several waves per SIMD; a
+  // lone wave per SIMD (WIDE) issues a step in a few tens of cycles, so it runs 4 steps ahead
+  // (rotating registers; 32 % PF == 0 keeps the rotation aligned across the two 32-step halves).
+  constexpr int PF = WIDE ? 4 : 1;
+  // (the codes run 2 PF steps ahead: a profile load's address is a code loaded PF steps earlier)
   int nTop = TOP0 ? C.top0 : C.bIn[0];
-  ProfV<RW> nP = load_prof<RW>(C.profLane + C.codeLane[0]);
-  int nCode = C.codeLane[1];
-  const uint16_t* cl = C.codeLane + 2;
-  const int* bi = C.bIn + 1;
+  int qTop[PF], qCode[PF];
+  ProfV<RW> qP[PF];
+#pragma unroll
+  for (int d = 0; d < PF; ++d) {
+    qTop[d] = TOP0 ? 0 : C.bIn[d];
+    qP[d] = load_prof<RW>(C.profLane + C.codeLane[d]);
+    qCode[d] = C.codeLane[PF + d];
+  }
+  const uint16_t* cl = C.codeLane + 2 * PF;
+  const int* bi = C.bIn + PF;
 #pragma unroll 1
   for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h, cl += BG_TRACE_BLK, bi += BG_TRACE_BLK) {
 #pragma unroll
     for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
       const int u = h * BG_TRACE_BLK + uu;
       const int t = t0 + u;
-      const int topIn = nTop;
-      const ProfV<RW> P = nP;
-      nP = load_prof<RW>(C.profLane + nCode);
-      nCode = cl[uu];
-      if constexpr (!TOP0) nTop = bi[uu];
+      const int slot = uu % PF;                               // constant after unrolling
+      const int topIn = TOP0 ? nTop : qTop[slot];
+      const ProfV<RW> P = qP[slot];
+      qP[slot] = load_prof<RW>(C.profLane + qCode[slot]);    // step u + PF
+      qCode[slot] = cl[uu];                                   // step u + 2 PF
+      // row above of step u + PF (past the 64-entry block at the chunk's end: never used)
+      if constexpr (!TOP0) qTop[slot] = bi[uu];
       const int topX = dpp_shr1(topIn, S.Xlast);             // M'(row above, j)
       // lane 0 keeps the DPP's old operand, the only lane whose row-0 input matters
       if constexpr (TOP0) nTop = topX + C.topStep;

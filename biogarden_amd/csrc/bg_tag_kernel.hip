@@ -266,12 +266,25 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       // publish.  LDS mailbox: the block's ds_writes precede the counter's in this wave's LDS
       // queue.  HBM: the chunk ends with the block store and R trace stores; at vmcnt(R) the
       // block store has completed (vector memory operations complete in order).
-      const int done = rho * nblk + (c < nblk ? c : nblk);
+      int done = rho * nblk + (c < nblk ? c : nblk);
       if (mailOut) {
         if (lane == 0) __hip_atomic_store(sProg + w, done, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else {
-        if constexpr (CKPT) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
+      } else if (s + 1 < nst) {                                    // a consumer reads HBM
+        if constexpr (CKPT) {
+          // interior chunks publish one block late instead of draining the stores: a chunk's
+          // vector memory operations are its R + 1 checkpoint stores, then the block store, so
+          // at vmcnt(R + 2) the previous chunk's block has completed (in-order completion); a
+          // drain per chunk stalled this wave (the last of a round, or of a WIDE workgroup) for
+          // the store round trip, and the strip pipeline behind it with it
+          if (!edge && c >= 2) {
+            asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R + 2) : "memory");
+            done -= 1;
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
+        } else {
+          asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
+        }
         if constexpr (WIDE) {
           if (lane == 0) __hip_atomic_store(gProg + gw, (uint32_t)done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
