@@ -37,6 +37,8 @@ def _raise_for(status, res):
         raise ReferencePanic("score closure index out of range", None)
     if status == _native.BG_REF_DIVERGENT:
         raise ReferencePanic("the reference SequenceAligner panics or hangs on this input", res)
+    if status == _native.BG_INTERNAL:
+        raise RuntimeError("biogarden_gpu: traceback recomputation timed out (internal error)")
 
 
 def _as_bytes(s):

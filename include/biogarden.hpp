@@ -379,6 +379,7 @@ class SequenceAligner {
       case BG_INVALID_ARGUMENT_RANGE: return BioError::InvalidArgumentRange;
       case BG_INVALID_INPUT_SIZE: return BioError::InvalidInputSize;
       case BG_UNSCORABLE: throw ReferencePanic("score closure panics on an input byte");
+      case BG_INTERNAL: throw std::runtime_error("biogarden_gpu: traceback recomputation timed out");
       default: throw ReferencePanic("the reference SequenceAligner panics or hangs on this input");
     }
   }
