@@ -364,3 +364,39 @@ def test_pipelined_executes_match_single():
     got = h.fetch()
     h.close()
     assert got == want
+
+
+# ------------------------------------------------------------------ asynchronous recomputation
+def _long_gap_pairs(rng):
+    """Paths that stress the traceback's chunk cache: a 3000-column insertion (the walk crosses
+    ~47 chunks of one strip: direct-mapped table collisions 16 chunks apart), a 2500-row deletion
+    (the walk climbs strips in one chunk column), and a diagonal pair for the prediction."""
+    base = rand_seq(rng, 6000, DNA)
+    ins = base[:3000] + rand_seq(rng, 3000, DNA) + base[3000:]
+    dele = base[:1500] + base[4000:]
+    return [(base, ins), (base, dele), (base, mutate(rng, base, DNA, 0.15))]
+
+
+@pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("global", -2, -2), ("overlap", -1, -1)])
+def test_traceback_async_matches_barriers_and_oracle(aligner, oracle, mode, a, b):
+    """The helper-wave recomputation (default) and the barrier form (BG_FIN_SYNC=1) give the
+    oracle's strings on long-gap paths, at the metric geometry and at a short-strip one."""
+    from biogarden_amd.alignment import score
+    rng = random.Random(0xA5C)
+    pairs = _long_gap_pairs(rng)
+    expect = [oracle.align(mode, s1, s2, "blosum62", a, b, exact=True) for s1, s2 in pairs]
+    try:
+        for R, W in ((8, 16), (2, 4)):
+            aligner.set_tuning(R, W)
+            for sync in (False, True):
+                if sync:
+                    os.environ["BG_FIN_SYNC"] = "1"
+                else:
+                    os.environ.pop("BG_FIN_SYNC", None)
+                res = aligner.align_batch(mode, pairs, score.blosum62, a, b)
+                for e, r in zip(expect, res):
+                    assert r.status in (0, 4), (R, W, sync, r.status)
+                    assert (e[1], e[2], e[3]) == (r[0], bytes(r[1].chain), bytes(r[2].chain)), (R, W, sync)
+    finally:
+        os.environ.pop("BG_FIN_SYNC", None)
+        aligner.set_tuning(0, 0)

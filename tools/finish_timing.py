@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Per-pair cycle breakdown of the finish kernel (BG_FINISH_TIMING=1): walk total, jumper blocks,
-misses (window loads / chunk recomputation).  python tools/finish_timing.py [pairs] [ckpt 0/1]"""
+misses (window loads / chunk recomputation), chunks recomputed.
+    python tools/finish_timing.py [pairs] [ckpt 0/1] [R W]"""
 import os
 import sys
 
@@ -14,6 +15,8 @@ ck = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 h = _native.Handle(0)
 h.set_pipeline(1)
 h.set_kernel_options(True, bool(ck))
+if len(sys.argv) > 4:
+    h.set_tuning(int(sys.argv[3]), int(sys.argv[4]))
 pairs = bench.make_pairs(npairs, 10000, 10000, bench.SEED)
 h.prepare("semiglobal", pairs, _native.builtin_scoring(_native.BG_BLOSUM62), -1, -2)
 h.execute()
