@@ -344,11 +344,14 @@ static void* fin_fn(const bg_aligner* h, int R) {
 // Finish workgroup of the checkpoint modes: waves (the walker + recompute helpers) and
 // recomputed-chunk slots.  Few pairs: 4 waves and every slot (the walk's latency is the step's
 // tail).  Many pairs: fewer waves and slots, so more pairs walk per CU at once (the walks are
-// latency-bound, one wave each).  BG_FIN_WAVES / BG_FIN_SLOTS override (experiments).
+// latency-bound).  BG_FIN_WAVES / BG_FIN_SLOTS override (experiments).
 static void fin_geom(const bg_aligner* h, size_t np, int* nw, int* nslots) {
   *nw = 4;
   *nslots = 0;
-  if ((h->ack || h->ckpt) && np > (size_t)h->cus * 2) { *nw = 1; *nslots = 2; }
+  // many pairs: two waves (walker + one recomputing helper at each miss) and three slots
+  // (tools/fin_geom_sweep.sh: one wave / two slots C2 1 266, C4 5 630, C5 2 274 GCUPS; two waves /
+  // three slots 1 269, 6 017, 2 396; four waves 1 298, 6 039, 2 123)
+  if ((h->ack || h->ckpt) && np > (size_t)h->cus * 2) { *nw = 2; *nslots = 3; }
   if (const char* e = std::getenv("BG_FIN_WAVES")) *nw = std::min(4, std::max(1, std::atoi(e)));
   if (const char* e = std::getenv("BG_FIN_SLOTS")) *nslots = std::max(0, std::atoi(e));
   if (*nslots && *nslots < *nw + 1) *nslots = *nw + 1;
