@@ -201,7 +201,7 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
   }
   const uint16_t* cl = C.codeLane + 2 * PF;
   const int* bi = C.bIn + PF;
-#pragma unroll 1
+#pragma unroll
   for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h, cl += BG_TRACE_BLK, bi += BG_TRACE_BLK) {
 #pragma unroll
     for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
