@@ -46,6 +46,18 @@ def test_no_gpu_means_loud_failure():
     raise AssertionError("bg_aligner_new succeeded without a GPU")
 
 
+def test_missing_library_is_loud(monkeypatch, tmp_path):
+    """No CPU fallback: an unbuilt library raises NativeUnavailable before any compute."""
+    from biogarden_amd import _native
+    monkeypatch.setattr(_native, "_LIB", None)
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "libbiogarden_gpu.so"))
+    try:
+        _native.lib()
+    except _native.NativeUnavailable:
+        return
+    raise AssertionError("lib() loaded without the built library")
+
+
 def test_library_is_gfx950():
     """The shipped code object targets gfx950 only (no multi-arch / CUDA shims)."""
     path = os.path.join(ROOT, "biogarden_amd", "libbiogarden_gpu.so")
