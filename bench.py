@@ -2,16 +2,33 @@
 """Benchmark: GCUPS of 10 kbp x 10 kbp affine-gap semiglobal alignment on MI355X.
 
 Metric (BASELINE.json): "GCUPS (billion DP cells/s), 10k x 10k affine-gap semiglobal, 1/2/4/8
-MI355X".  Workload per GPU: 256 synthetic uniform-DNA pairs of 10,000 x 10,000, semiglobal,
-BLOSUM62, gap open -1 / extend -2 (the reference's own config-1 parameters,
-examples/from_file.rs:19-32).  One step = one pass of the hot path over the batch with the
-inputs resident in HBM: DP kernel (scores + trace) -> end-cell search -> traceback writing both
-aligned strings (aligner.rs:351-435).  Every rank aligns its own 256 pairs (weak scaling: the
-pairs are independent, no data-path collective); after the timed region the per-rank results
-are gathered to rank 0 over RCCL (reported as gather_ms).
+MI355X".  Workload M per GPU: 256 synthetic uniform-DNA pairs of
+10 000 x 10 000, semiglobal, BLOSUM62, gap open -1 / extend -2 (the reference's own config-1
+parameters, examples/from_file.rs:19-32).  With open >= extend the Gotoh DP provably collapses to
+linear gaps, so the line also carries `affine`: the same pairs with open -11 /
+extend -1, the genuinely affine three-matrix DP and the reference's one-cell-late X/Y traceback.
+
+One step = one pass of the hot path over the batch with the inputs resident in HBM: DP kernel
+-> end-cell search -> traceback writing both aligned strings (aligner.rs:351-435), three
+pipeline slots (the traceback of step k overlaps the DP of step k+1).  Every rank aligns its own
+256 pairs (weak scaling: the pairs are independent, no data-path collective); after the timed
+region the per-rank packed results are gathered to rank 0 over RCCL (gather_ms).  `--shard`
+instead LPT-shards one batch of 256 pairs over the ranks (strong scaling, §8(d)'s phrasing).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Fields beyond the driver's contract:
+  roofline        the DP kernel (the dominant one) against §8(d)'s algorithmic bytes
+                  (0.25 B/cell for open >= extend, 0.5 for open < extend, plus the residues),
+                  HBM peak 8 TB/s; `bound` names the roof that binds (VALU issue) and `valu`
+                  its fraction: PMC-measured VALU instructions x 64 lanes / kernel time against
+                  256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (MI355X_MICROARCH.md)
+  host_to_host    PCIe-inclusive rate: residues uploaded from host buffers, aligned strings
+                  downloaded to host buffers, two handles ping-ponged so one batch's upload and
+                  download overlap the other's kernels (never `value`)
+  cpu_baseline    the oracle (oracle/refcpu.c: the reference's six full matrices, its loop order,
+                  one reused aligner per thread) on this host's cores, plus a 1-core rate and C1
 """
 import argparse
 import json
@@ -19,28 +36,68 @@ import os
 import sys
 import time
 
-import numpy as np
-
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
-# int32 VALU: a wave64 instruction occupies its SIMD ~4 cycles (v_max3 / v_add_sdwa / DPP measured
-# 4.4 at 4 waves per SIMD, profiles/r01/micro_valu_rates.txt), i.e. 16 lanes per SIMD per cycle
-VALU_PEAK_OPS = 256 * 4 * 16 * 2.4e9   # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz int32 lane-ops/s
-VALU_CYC_PER_INSTR = 4.4
-SEED = 0xB10A11F0 + 5          # seed = 0xB10A11F0 + config index (metric = 5)
+from tools import workloads  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0                     # MI355X_MICROARCH.md "HBM3E peak BW 8.0 TB/s spec"
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9  # guide: a wave64 VALU instruction issues over 2 cycles
+VALU_CYC_PER_INSTR = 4.4                   # measured issue cost of the step's v_max3 / v_add_sdwa /
+                                           # DPP mix (profiles/r01/micro_valu_rates.txt)
+MEASURED_ISSUE_LANE_OPS = 256 * 4 * 64 / VALU_CYC_PER_INSTR * 2.4e9
+SEED = workloads.SEED0 + 5                 # seed = 0xB10A11F0 + config index (M = 5)
+METRIC = "GCUPS (billion DP cells/s), 10k×10k affine-gap semiglobal, 1/2/4/8 MI355X"
 
 
 def make_pairs(npairs, n1, n2, seed):
-    rng = np.random.default_rng(seed)
-    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
-    pairs = []
-    for _ in range(npairs):
-        s1 = acgt[rng.integers(0, 4, n1)].tobytes()
-        s2 = acgt[rng.integers(0, 4, n2)].tobytes()
-        pairs.append((s1, s2))
-    return pairs
+    return workloads.metric_pairs(npairs, n1, n2, seed)
+
+
+# ------------------------------------------------------------------ host description
+
+
+def host_info():
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cpus"] = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        info["affinity_cpus"] = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    info["cgroup_cpu_quota"] = quota
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["cpu_model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        with open("/proc/meminfo") as f:
+            for line in f:
+                if line.startswith(("MemTotal", "MemAvailable")):
+                    k, v = line.split(":")
+                    info[k.strip().lower() + "_gib"] = round(int(v.split()[0]) / 2 ** 20, 1)
+    except OSError:
+        pass
+    return info
+
+
+def usable_cores(info):
+    """Threads the CPU baseline runs on: every CPU this process may use (affinity), bounded by
+    the cgroup's CPU quota when one is set (threads beyond it only time-share)."""
+    n = info.get("affinity_cpus") or 1
+    if info.get("cgroup_cpu_quota"):
+        n = min(n, max(1, int(info["cgroup_cpu_quota"])))
+    return max(1, n)
 
 
 def cpu_baseline(pairs, mode, a, b, threads):
@@ -48,8 +105,10 @@ def cpu_baseline(pairs, mode, a, b, threads):
     from oracle import refcpu
     secs, scores, sts = refcpu.align_batch(mode, pairs, "blosum62", a, b, nthreads=threads,
                                            exact=False)
-    cells = sum(len(x) * len(y) for x, y in pairs)
-    return cells / secs / 1e9, secs, scores, sts
+    return workloads.cells(pairs) / secs / 1e9, secs, scores, sts
+
+
+# ------------------------------------------------------------------ PMC summaries
 
 
 def load_pmc(workload):
@@ -65,21 +124,141 @@ def load_pmc(workload):
         return {}
 
 
-# Register-only ceiling of the tagged full-trace kernel's step (tools/micro/tag_step.hip on MI355X,
-# 16 waves per CU, profiles/r01/micro_tag_step.txt): 5R + 2 instructions per 64R cells.
-TAG_REGISTER_CEILING = {4: 6.94e12, 5: 6.60e12, 8: 7.01e12, 10: 6.94e12}
+def workload_name(mode, npairs, n1, n2, a, b):
+    return "%s_%dx%dx%d_blosum62_o%d_e%d" % (mode, npairs, n1, n2, -a, -b)
 
 
-def register_ceiling(st):
-    """DP cells/s if every SIMD issued the kernel's step instructions back to back at
-    VALU_CYC_PER_INSTR: score-only linear step 2R + 2 instructions per 64R cells (v_add_sdwa +
-    v_max3 per cell, DPP + profile address per step); tagged full trace from the micro-benchmark."""
-    R = st["R"]
-    if st["tagged"] and st["checkpoint"]:
-        return 256 * 4 * 2.4e9 / VALU_CYC_PER_INSTR * 64 * R / (2 * R + 2), "2R+2 per 64R cells"
-    if st["tagged"] and R in TAG_REGISTER_CEILING:
-        return TAG_REGISTER_CEILING[R], "micro-benchmark (5R+2 per 64R cells)"
-    return None, None
+def kernel_name(st):
+    if st["tagged"]:
+        return "bg_dp_tag_kernel<R=%d,%s,ckpt=%d>" % (st["R"], "WIDE" if st["wide"] else "strips",
+                                                     st["checkpoint"])
+    if st["checkpoint"]:
+        return "bg_dp_aff_kernel<R=%d,local=%d>" % (st["R"], st["local"])
+    return "bg_dp_kernel<R=%d>" % st["R"]
+
+
+def roofline(st, cells, dp_ms, workload, a, b):
+    """§8(d): algorithmic bytes per cell 0.25 (open >= extend: 2-bit m_trace) or 0.5 (4-bit trace)
+    plus the residues, over the DP kernel's event-timed launch; VALU from the PMC summary."""
+    bpc = 0.25 if a >= b else 0.5
+    algo = cells * bpc + st["residue_bytes"]
+    achieved = algo / (dp_ms * 1e-3) / 1e9 if dp_ms > 0 else 0.0
+    pmc = load_pmc(workload)
+    same = pmc.get("geometry") == [str(st["R"]), str(st["waves"])]
+    traffic = pmc.get("hbm_bytes_per_launch") if same else None
+    cps = cells / (dp_ms * 1e-3) if dp_ms > 0 else 0.0
+    valu = {"peak_lane_ops_per_s": VALU_PEAK_LANE_OPS,
+            "peak_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}
+    insts = pmc.get("raw_counters", {}).get("SQ_INSTS_VALU") if same else None
+    if insts:
+        ipc = insts * 64.0 / cells
+        valu.update({"instr_per_cell": round(ipc, 3),
+                     "lane_ops_per_s": round(ipc * cps, -9),
+                     "frac": round(ipc * cps / VALU_PEAK_LANE_OPS, 4),
+                     # second figure: against the measured ~4.4-cycle issue of this mix
+                     "frac_of_measured_issue": round(ipc * cps / MEASURED_ISSUE_LANE_OPS, 4),
+                     "pmc_source": "profiles/pmc_%s.json" % workload})
+    return {"bound": "valu", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "frac_basis": "HBM roofline of SURVEY 8(d): (%.2f B/cell + residues) / DP kernel time "
+                          "/ 8 TB/s; the binding roof is VALU issue (see valu.frac)" % bpc,
+            "algorithmic_bytes_per_launch": int(algo),
+            "traffic_source": ("profiles/pmc_%s.json" % workload) if traffic else None,
+            "kernel": kernel_name(st), "kernel_ms": round(dp_ms, 4), "valu": valu}
+
+
+# ------------------------------------------------------------------ timed runs
+
+
+def timed(h, steps, warmup, barrier):
+    for _ in range(warmup):
+        h.execute()
+    h.synchronize()
+    barrier()
+    h.profile_begin()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        h.execute()
+    h.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    dp_ms, fin_ms, _ = h.profile_end()
+    return elapsed, dp_ms, fin_ms
+
+
+def host_to_host(native, pairs, sc, mode, a, b, device, rounds=6, pipeline=3):
+    """PCIe-inclusive throughput: per round one batch is prepared from host buffers (validation,
+    residue coding, H2D), executed, and fetched (D2H, aligned strings in host buffers).  Two
+    handles alternate so that batch k+1's upload runs while batch k is on the GPU and batch k's
+    download while k+1 is."""
+    hs = [native.Handle(device) for _ in range(2)]
+    for x in hs:
+        x.set_pipeline(pipeline)
+    try:
+        hs[0].prepare(mode, pairs, sc, a, b)          # warm the arenas of both handles
+        hs[0].execute()
+        hs[0].fetch()
+        hs[1].prepare(mode, pairs, sc, a, b)
+        hs[1].execute()
+        hs[1].fetch()
+        t_prep = t_fetch = 0.0
+        t0 = time.perf_counter()
+        hs[0].prepare(mode, pairs, sc, a, b)
+        hs[0].execute()
+        for r in range(1, rounds + 1):
+            cur, prev = hs[r % 2], hs[(r - 1) % 2]
+            if r < rounds:
+                tp = time.perf_counter()
+                cur.prepare(mode, pairs, sc, a, b)
+                cur.execute()
+                t_prep += time.perf_counter() - tp
+            tf = time.perf_counter()
+            prev.fetch_raw()
+            t_fetch += time.perf_counter() - tf
+        secs = time.perf_counter() - t0
+    finally:
+        for x in hs:
+            x.close()
+    cells = workloads.cells(pairs)
+    return {"gcups": round(cells * rounds / secs / 1e9, 2), "rounds": rounds,
+            "seconds_per_batch": round(secs / rounds, 5),
+            "host_prepare_s_per_batch": round(t_prep / max(rounds - 1, 1), 5),
+            "fetch_wait_s_per_batch": round(t_fetch / rounds, 5),
+            "covers": "bg_batch_prepare (validation, residue coding, H2D) + execute + "
+                      "bg_batch_fetch (D2H, aligned strings in caller buffers); two handles "
+                      "ping-ponged"}
+
+
+def cpu_section(pairs, gpu_scores, mode, a, b, info, pairs_multi, pairs_one):
+    """Rank 0 at N = 1: the oracle on every usable core over a bounded sample of M, on 1 core
+    over >= 8 pairs, and C1 (the reference's own example) on 1 core."""
+    threads = usable_cores(info)
+    nm = min(len(pairs), max(pairs_multi, threads))
+    sample = pairs[:nm]
+    rate, secs, cscores, _ = cpu_baseline(sample, mode, a, b, threads)
+    one = pairs[:pairs_one]
+    rate1, secs1, cs1, _ = cpu_baseline(one, mode, a, b, 1)
+    out = {"value": round(rate, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
+           "sample": "%d of the %d M pairs (10000x10000), oracle/refcpu.c reference-faithful "
+                     "(six full matrices, 15 B/cell), one reused aligner per thread, %d threads, "
+                     "%.1f s wall" % (nm, len(pairs), threads, secs),
+           "scores_match_gpu": "%d/%d" % (sum(int(x == y) for x, y in zip(cscores, gpu_scores)), nm),
+           "one_core": {"value": round(rate1, 4), "pairs": len(one), "seconds": round(secs1, 2),
+                        "scores_match_gpu": "%d/%d" % (
+                            sum(int(x == y) for x, y in zip(cs1, gpu_scores)), len(one))},
+           "host": info}
+    try:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from conftest import REF_FIX, read_fasta
+        recs = read_fasta(os.path.join(REF_FIX, "input", "semiglobal_alignment.fasta"))
+        c1 = [(recs[0][1], recs[1][1])]
+        r1, s1_, sc1, _ = cpu_baseline(c1, "semiglobal", -1, -2, 1)
+        out["C1_one_core"] = {"value": round(r1, 4), "seconds": round(s1_, 3), "score": sc1[0],
+                              "cells": workloads.cells(c1),
+                              "config": "semiglobal_alignment.fasta 9559x8457, blosum62 -1/-2"}
+    except (OSError, IndexError, ImportError):
+        pass
+    return out
 
 
 def main():
@@ -93,13 +272,19 @@ def main():
     ap.add_argument("--mode", default="semiglobal")
     ap.add_argument("--open", type=int, default=-1)
     ap.add_argument("--extend", type=int, default=-2)
+    ap.add_argument("--affine-open", type=int, default=-11)
+    ap.add_argument("--affine-extend", type=int, default=-1)
     ap.add_argument("--R", type=int, default=0)
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--pipeline", type=int, default=3,
                     help="slots: >= 2 lets the traceback of step k overlap the DP of step k+1 "
                          "(two HIP streams); 3 absorbs traceback times that vary around the DP's")
-    ap.add_argument("--cpu-pairs", type=int, default=16)
+    ap.add_argument("--shard", action="store_true",
+                    help="strong scaling: LPT-shard one batch of --pairs over the ranks")
+    ap.add_argument("--cpu-pairs", type=int, default=32, help="M pairs for the all-core CPU rate")
+    ap.add_argument("--cpu-one-pairs", type=int, default=8, help="M pairs for the 1-core CPU rate")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-affine", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host timing")
     args = ap.parse_args()
@@ -114,52 +299,54 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    from biogarden_amd import _native
-
-    h = _native.Handle(local_rank)
-    if args.R or args.waves:
-        h.set_tuning(args.R, args.waves)
-    h.set_pipeline(args.pipeline)
-    pairs = make_pairs(args.pairs, args.len1, args.len2, SEED + 1000003 * rank)
-    sc = _native.builtin_scoring(_native.BG_BLOSUM62)
-    h.prepare(args.mode, pairs, sc, args.open, args.extend)
-    st = h.stats()
-    cells = st["cells"]
-
-    for _ in range(args.warmup):
-        h.execute()
-    h.synchronize()
+    from biogarden_amd import _native, shard
 
     def barrier():
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    h.profile_begin()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        h.execute()
-    h.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    dp_ms, fin_ms, nexec = h.profile_end()
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    def max_over_ranks(x):
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    ms_per_step = elapsed / args.steps * 1e3
-    total_cells = cells * world
-    gcups = total_cells * args.steps / elapsed / 1e9
+        return float(t.item())
 
-    # ---- results: RCCL gather of every rank's packed results to rank 0
+    h = _native.Handle(local_rank)
+    if args.R or args.waves:
+        h.set_tuning(args.R, args.waves)
+    h.set_pipeline(args.pipeline)
+    if args.shard:
+        allpairs = make_pairs(args.pairs, args.len1, args.len2, SEED)
+        shards = shard.lpt_shards([(len(x), len(y)) for x, y in allpairs], world)
+        pairs = [allpairs[p] for p in shards[rank]]
+    else:
+        pairs = make_pairs(args.pairs, args.len1, args.len2, SEED + 1000003 * rank)
+    sc = _native.builtin_scoring(_native.BG_BLOSUM62)
+
+    # ---- M: the metric workload
+    h.prepare(args.mode, pairs, sc, args.open, args.extend)
+    st = h.stats()
+    cells = st["cells"]
+    elapsed, dp_ms, fin_ms = timed(h, args.steps, args.warmup, barrier)
+    elapsed = max_over_ranks(elapsed)
+    if dist is not None:
+        t = torch.tensor([float(cells)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t)
+        total_cells = float(t.item())
+    else:
+        total_cells = float(cells)
+    gcups = total_cells * args.steps / elapsed / 1e9
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- results: RCCL gather of every rank's packed results to rank 0 (after the timed region)
     gather_ms = None
     results0 = None
     nbytes = h.export_size()
     local = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
     h.export_to(local.data_ptr(), nbytes)
     if dist is not None and not args.no_gather:
-        from biogarden_amd import shard
         barrier()
         tg = time.perf_counter()
         packed = shard.gather_packed(local, dist, dst=0)
@@ -169,71 +356,54 @@ def main():
             results0 = [_native.decode_export(b) for b in packed]
     else:
         results0 = [_native.decode_export(local.cpu().numpy().tobytes())]
+    workload = workload_name(args.mode, args.pairs, args.len1, args.len2, args.open, args.extend)
+    roof = roofline(st, cells, dp_ms, workload, args.open, args.extend)
+    roof["finish_ms"] = round(fin_ms, 4)
+
+    # ---- MA: the same pairs with a genuinely affine gap model (open < extend)
+    aff = None
+    if not args.no_affine:
+        a2, b2 = args.affine_open, args.affine_extend
+        h.prepare(args.mode, pairs, sc, a2, b2)
+        sta = h.stats()
+        ea, dpa, fina = timed(h, max(2, args.steps // 2), max(1, args.warmup // 2), barrier)
+        ea = max_over_ranks(ea)
+        na = max(2, args.steps // 2)
+        resa = h.fetch_raw()
+        wla = workload_name(args.mode, args.pairs, args.len1, args.len2, a2, b2)
+        ra = roofline(sta, sta["cells"], dpa, wla, a2, b2)
+        ra["finish_ms"] = round(fina, 4)
+        aff = {"workload": wla, "value": round(total_cells * na / ea / 1e9, 3), "unit": "GCUPS",
+               "steps": na, "ms_per_step": round(ea / na * 1e3, 4),
+               "gap_open": a2, "gap_extend": b2,
+               "kernel": {"R": sta["R"], "waves": sta["waves"], "affine": sta["affine"],
+                          "checkpoint": sta["checkpoint"], "fin_waves": sta["fin_waves"],
+                          "fin_slots": sta["fin_slots"]},
+               "roofline": ra, "all_status_ok": all(s == 0 for s in resa["status"])}
 
     # ---- host-to-host rate (not `value`): host buffers in, aligned strings back on the host
     h2h = None
     if not args.no_h2h:
-        h.set_pipeline(1)
-        torch.cuda.synchronize()
-        th = time.perf_counter()
-        h.prepare(args.mode, pairs, sc, args.open, args.extend)
-        h.execute()
-        h.fetch()
-        h2h_s = time.perf_counter() - th
-        h2h = {"gcups": round(cells / h2h_s / 1e9, 3), "seconds": round(h2h_s, 4),
-               "covers": "bg_batch_prepare (validation, residue coding, H2D) + execute + "
-                         "bg_batch_fetch (D2H of results and aligned strings), one call"}
+        h2h = host_to_host(_native, pairs, sc, args.mode, args.open, args.extend, local_rank,
+                           pipeline=args.pipeline)
 
     if rank != 0:
+        h.close()
         if dist is not None:
             dist.destroy_process_group()
         return
 
     ok_status = all(r["status"] == 0 for rr in results0 for r in rr)
+    gpu_scores = [r["score"] for r in results0[0]]
 
-    # ---- roofline of the DP kernel (algorithmic bytes per launch / event-timed duration)
-    if st["checkpoint"]:
-        # score-only DP: per lane and 64-step chunk R + 1 checkpoint ints, per strip its last row
-        bytes_per_cell = (4.0 * (st["R"] + 1) + 4.0) / (64.0 * st["R"])
-    else:
-        bytes_per_cell = 0.25 if st["affine"] == 0 else 0.5    # the 2-bit (4-bit) trace
-    algo_bytes = cells * bytes_per_cell + st["residue_bytes"]
-    achieved = algo_bytes / (dp_ms * 1e-3) / 1e9 if dp_ms > 0 else 0.0
-    workload = "semiglobal_%dx%dx%d_blosum62_o%d_e%d" % (args.pairs, args.len1, args.len2,
-                                                          -args.open, -args.extend)
-    pmc = load_pmc(workload)
-    same_geom = pmc.get("geometry") == [str(st["R"]), str(st["waves"])]
-    traffic = pmc.get("hbm_bytes_per_launch") if same_geom else None
-    cells_per_s = cells / (dp_ms * 1e-3) if dp_ms > 0 else 0.0
-    valu = {"lane_ops_peak": VALU_PEAK_OPS}
-    insts = pmc.get("raw_counters", {}).get("SQ_INSTS_VALU") if same_geom else None
-    if insts:
-        per_cell = insts * 64.0 / cells
-        valu.update({"instr_per_cell_measured": round(per_cell, 3),
-                     "lane_ops_achieved": per_cell * cells_per_s,
-                     "frac_of_lane_peak": round(per_cell * cells_per_s / VALU_PEAK_OPS, 4)})
-    ceil_, how = register_ceiling(st)
-    if ceil_:
-        valu.update({"register_ceiling_cells_per_s": round(ceil_, -9), "register_ceiling_model": how,
-                     "frac_of_register_ceiling": round(cells_per_s / ceil_, 4)})
-
-    # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0 only)
+    # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0, N = 1)
     cpu = None
     if not args.no_cpu and world == 1:
-        threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)),
-                             os.cpu_count() or 1))
-        sample = pairs[:max(1, min(args.cpu_pairs, len(pairs)))]
-        rate, secs, cscores, csts = cpu_baseline(sample, args.mode, args.open, args.extend, threads)
-        gscores = [r["score"] for r in results0[0][:len(sample)]]
-        cpu = {"value": round(rate, 4), "unit": "GCUPS", "cores": threads, "kind": "port",
-               "sample": "%d of the %d pairs (%dx%d), oracle/refcpu.c reference-faithful full "
-                         "matrices, one aligner per thread, %.1f s wall" % (
-                             len(sample), len(pairs), args.len1, args.len2, secs),
-               "scores_match_gpu": "%d/%d" % (sum(int(x == y) for x, y in zip(cscores, gscores)),
-                                               len(sample))}
+        cpu = cpu_section(pairs, gpu_scores, args.mode, args.open, args.extend, host_info(),
+                          args.cpu_pairs, args.cpu_one_pairs)
 
     line = {
-        "metric": "GCUPS (billion DP cells/s), 10k×10k affine-gap semiglobal, 1/2/4/8 MI355X",
+        "metric": METRIC,
         "value": round(gcups, 3),
         "unit": "GCUPS",
         "n_gpus": world,
@@ -241,32 +411,29 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.shard else "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic (uniform DNA, numpy PCG64 seed 0x%X + 1000003*rank)" % SEED,
-        "config": {"workload": workload, "pairs_per_gpu": args.pairs, "len1": args.len1,
+        "data": "synthetic (uniform DNA, numpy PCG64 seed 0x%X%s)" % (
+            SEED, "" if args.shard else " + 1000003*rank"),
+        "config": {"workload": workload, "pairs_per_gpu": len(pairs), "len1": args.len1,
                    "len2": args.len2, "mode": args.mode, "scoring": "blosum62",
                    "gap_open": args.open, "gap_extend": args.extend,
                    "kernel": {"R": st["R"], "waves": st["waves"], "affine": st["affine"],
                               "tagged": st["tagged"], "checkpoint": st["checkpoint"],
-                              "dna_profile": st["dna"], "pipeline": args.pipeline},
-                   "parallelism": "dp%d (independent pairs per rank)" % world},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "algorithmic_bytes_per_launch": int(algo_bytes),
-                     "traffic_source": ("profiles/pmc_%s.json" % workload) if traffic else None,
-                     "kernel": ("bg_dp_tag_kernel<ckpt>" if st["checkpoint"] else "bg_dp_tag_kernel")
-                               if st["tagged"] else "bg_dp_kernel",
-                     "kernel_ms": round(dp_ms, 4), "finish_ms": round(fin_ms, 4),
-                     "valu": valu},
+                              "dna_profile": st["dna"], "pipeline": args.pipeline,
+                              "fin_waves": st["fin_waves"], "fin_slots": st["fin_slots"]},
+                   "parallelism": "dp%d (%s)" % (world, "one batch LPT-sharded" if args.shard
+                                                 else "independent pairs per rank")},
+        "roofline": roof,
         "cpu_baseline": cpu,
+        "affine": aff,
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         "host_to_host": h2h,
         "all_status_ok": ok_status,
     }
     print(json.dumps(line))
+    h.close()
     if dist is not None:
         dist.destroy_process_group()
 

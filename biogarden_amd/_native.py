@@ -21,7 +21,7 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
            "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
            "bg_set_pipeline", "bg_set_kernel_options", "bg_edit_distance_batch",
-           "bg_lcs_batch"]
+           "bg_lcs_batch", "bg_aligner_buffer_size"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -50,7 +50,8 @@ class BgStats(ctypes.Structure):
                 ("local", ctypes.c_int32), ("npairs", ctypes.c_int32),
                 ("wide", ctypes.c_int32), ("workgroups", ctypes.c_int32),
                 ("checkpoint", ctypes.c_int32),
-                ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float)]
+                ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float),
+                ("fin_waves", ctypes.c_int32), ("fin_slots", ctypes.c_int32)]
 
 
 _LIB = None
@@ -89,6 +90,8 @@ def lib():
     L.bg_batch_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
                                  ctypes.c_size_t]
     L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
+    L.bg_aligner_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                                         ctypes.POINTER(ctypes.c_size_t)]
     L.bg_set_tuning.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     L.bg_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.bg_set_kernel_options.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -197,6 +200,26 @@ class Handle:
                         "start": (r.start1, r.start2)})
         return out
 
+    def fetch_raw(self):
+        """bg_batch_fetch into handle-owned ctypes buffers, without per-pair Python objects:
+        {"status": [..], "score": [..], "offset": [..], "len": [..], "out1": buf, "out2": buf}
+        (the buffers are reused by the next fetch_raw)."""
+        n = self._npairs
+        need = max(self._total, 1)
+        if getattr(self, "_raw_cap", 0) < need or getattr(self, "_raw_n", 0) < max(n, 1):
+            self._raw_res = (BgPairResult * max(n, 1))()
+            self._raw_o1 = (ctypes.c_uint8 * need)()
+            self._raw_o2 = (ctypes.c_uint8 * need)()
+            self._raw_cap = need
+            self._raw_n = max(n, 1)
+        check(lib().bg_batch_fetch(self._p, self._raw_res, self._raw_o1, self._raw_o2, self._total))
+        res = self._raw_res
+        return {"status": [res[p].status for p in range(n)],
+                "score": [res[p].score for p in range(n)],
+                "offset": [res[p].offset for p in range(n)],
+                "len": [res[p].len for p in range(n)],
+                "out1": self._raw_o1, "out2": self._raw_o2}
+
     def align_batch(self, mode, pairs, scoring, a, b):
         self.prepare(mode, pairs, scoring, a, b)
         self.execute()
@@ -241,6 +264,12 @@ class Handle:
         check(lib().bg_lcs_batch(self._p, n, a1, n1, a2, n2, buf, cap, off, ln))
         raw = bytes(buf)
         return [raw[off[p]:off[p] + ln[p]] for p in range(n)]
+
+    def buffer_size(self):
+        """The reference aligner's scratch dims this handle models (aligner.rs:30)."""
+        r, c = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib().bg_aligner_buffer_size(self._p, ctypes.byref(r), ctypes.byref(c)))
+        return r.value, c.value
 
     def stats(self):
         st = BgStats()

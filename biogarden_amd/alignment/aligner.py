@@ -109,5 +109,11 @@ class SequenceAligner:
     def stats(self):
         return self._h.stats()
 
+    @property
+    def buffer_size(self):
+        """(rows, cols) of the reference aligner's scratch after the calls so far (aligner.rs:30):
+        (1024, 1024) when new, (len1+1, len2+1) after a call that did not fit (:92-94)."""
+        return self._h.buffer_size()
+
     def close(self):
         self._h.close()

@@ -31,24 +31,40 @@ struct BgPair {
   int32_t caller;      // caller's pair index
   int32_t wg_count;    // tagged kernel, WIDE mode: workgroups working on this pair (else 1)
   uint32_t prog_off;   // WIDE mode: offset of the pair's wg_count*W progress counters in gprog
-  int32_t reserved;
+  int32_t buf_rows;    // the reference aligner's scratch when this pair's call starts (rows, cols)
+  int32_t buf_cols;
 };
 
-// Would a freshly constructed reference SequenceAligner (1024x1024 scratch, aligner.rs:44-55)
-// panic, hang or answer from stale scratch on this pair?  Exact-size semantics differ from it
-// only when it does not resize (both lengths <= 1024) and either indexes row/column 1024 or its
-// end-cell fold reaches cells beyond the pair's region (DESIGN.md "Buffer semantics").
-__host__ __device__ inline bool bg_ref_fresh_divergent(int mode, long n1, long n2, int score) {
-  if (n1 > 1024 || n2 > 1024) return false;  // resized to exactly (n1+1, n2+1)
-  const bool e1 = n1 == 1024, e2 = n2 == 1024;
+// Would the reference SequenceAligner, whose scratch is rows x cols when this call starts
+// (1024 x 1024 for SequenceAligner::new, aligner.rs:44-55; resize_buffers(len1 + 1, len2 + 1)
+// whenever len1 > rows || len2 > cols, :92-94, 594-602), panic, hang or answer from stale scratch
+// on this pair?  Exact-size semantics differ from it only when it does not resize and either
+// indexes row `rows` / column `cols` (ndarray bounds panic) or its end-cell fold reaches cells
+// beyond the pair's region (DESIGN.md "Buffer semantics").  Whether it hangs or
+// answers from stale scratch there depends on the call history; both are flagged.
+__host__ __device__ inline bool bg_ref_divergent(int mode, long n1, long n2, int score, long rows,
+                                                 long cols) {
+  if (n1 > rows || n2 > cols) {
+    // resized to exactly (n1+1, n2+1); the border writes row0[1] / col0[1] (global, :98-104;
+    // fitting, :235) then index a dimension of length 1 when a sequence is empty
+    if (mode == BGK_GLOBAL) return n1 == 0 || n2 == 0;
+    if (mode == BGK_FITTING) return n2 == 0;
+    return false;
+  }
+  const bool e1 = n1 == rows, e2 = n2 == cols;
   switch (mode) {
-    case BGK_GLOBAL: return e1 || e2;
+    case BGK_GLOBAL: return e1 || e2 || rows < 2 || cols < 2;
     case BGK_LOCAL: return (e1 || e2) && n1 > 0 && n2 > 0;
-    case BGK_FITTING: return e2 || (e1 && n2 > 0) || (score < 0 && n1 + 1 < 1024);
-    case BGK_OVERLAP: return e1 || e2 || (score <= 0 && n2 + 1 < 1024);
-    default: return e1 || e2 || (score == 0 && n2 + 1 < 1024);
+    case BGK_FITTING: return e2 || cols < 2 || (e1 && n2 > 0) || (score < 0 && n1 + 1 < rows);
+    case BGK_OVERLAP: return e1 || e2 || (score <= 0 && n2 + 1 < cols);
+    default: return e1 || e2 || (score == 0 && n2 + 1 < cols);
   }
 }
+
+// Checkpoint tracebacks key a recomputed chunk by (strip << 20 | chunk << 4 | slot) in 32 bits
+// (bg_finish.h ckMap): pairs beyond these limits take the full-trace kernels (bg_host.cpp).
+#define BG_CK_MAX_STRIPS 4096
+#define BG_CK_MAX_CHUNKS 65536
 
 // Per-pair result written by the finish kernel.
 struct BgResult {
@@ -121,7 +137,9 @@ struct BgFinishArgs {
 enum {
   BG_FIN_SCORE_ONLY = 2,   // end cell and score only, no traceback (analysis::seq::edit_distance)
   BG_FIN_LCS = 4,          // LCS tie rule in the recomputed trace; out2 receives the op codes
-  BG_FIN_SYNC = 8          // linear checkpoint traceback: recompute at barriers (BG_FIN_SYNC=1, A/B)
+  BG_FIN_SYNC = 8,         // linear checkpoint traceback: recompute at barriers (BG_FIN_SYNC=1, A/B)
+  BG_FIN_SELFSERVE = 16    // asynchronous traceback: the walker recomputes every miss itself at
+                           // once (tests the forward-progress path; BG_FIN_SELFSERVE=1)
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

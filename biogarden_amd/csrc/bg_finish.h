@@ -158,6 +158,8 @@ constexpr int kAboveRows = 128;
 #define BG_SPEC_DEPTH 2
 #endif
 constexpr int kSpecDepth = BG_SPEC_DEPTH;
+// asynchronous recomputation: polls of the chunk map before the walker serves its own request
+constexpr int kSelfPolls = 4096;
 __device__ __forceinline__ int ck_map_idx(int s, int c) { return ((s & 15) << 4) | (c & 15); }
 
 // this wave-lane's profile entries for strip s, built by the whole workgroup
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         if (colcase) { ei = (int)(0xFFFFFFFFu - (unsigned)ka); ej = n2; score = mc; }
         else { ei = n1; ej = (int)(unsigned)kb; score = mr; }
       }
-      sh[0] = ei; sh[1] = ej; sh[2] = score; sh[3] = colcase;
+      sh[0] = ei; sh[1] = ej; sh[2] = score; sh[3] = colcase; sh[9] = 0;
     }
   }
   __syncthreads();
@@ -474,6 +476,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     }
   }
   u64 tJump = 0, tMiss = 0, nJump = 0, nMiss = 0, nRec = 0;   // BG_FINISH_TIMING instrumentation
+  u64 nSelf = 0;                                            // chunks the walker recomputed itself
+  int lastReqS = -1, lastReqB = -1, sameReq = 0;            // barrier path: repeated requests
   const u64 tWalk0 = __builtin_readcyclecounter();
 
   // ---- linear checkpoint traceback, asynchronous recomputation.  The helper waves recompute
@@ -740,14 +744,58 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
               __hip_atomic_store(&sh[33], key, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             const unsigned* me = &ckMap[ck_map_idx(reqS, reqB0)];
+            // Forward progress: after kSelfPolls polls without a helper taking the request (all
+            // busy prefetching), the walker claims a slot under the same lock and recomputes the
+            // chunk itself.  A chunk already being filled is only waited for (its filler always
+            // finishes); the bound below is a last-resort guard that no schedule reaches.
+            const int selfPolls = (F.flags & BG_FIN_SELFSERVE) ? 0 : kSelfPolls;
             int it = 0;
+            bool got = false;
             for (;; ++it) {
               const unsigned e = __hip_atomic_load(me, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-              if (e != 0xFFFFFFFFu && (int)(e >> 4) == key) break;
-              if (it > (1 << 22)) break;                   // no helper answered: give up loudly
+              if (e != 0xFFFFFFFFu && (int)(e >> 4) == key) { got = true; break; }
+              if (it >= selfPolls && (it - selfPolls) % 64 == 0) {
+                int zz = -1;
+                if (lane == 0) {
+                  while (__hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+                    __builtin_amdgcn_s_sleep(1);
+                  const unsigned e2 = __hip_atomic_load(me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                  bool busy = e2 != 0xFFFFFFFFu && (int)(e2 >> 4) == key;     // published meanwhile
+                  for (int z = 0; z < nSlots; ++z) busy |= (sh[48 + z] != 0 && sh[40 + z] == key);
+                  if (!busy) {
+                    // any slot not being filled: the walker reads nothing while it waits
+                    for (int z = 0; z < nSlots && zz < 0; ++z) if (!sh[48 + z]) zz = z;
+                    if (zz >= 0) {
+                      const int oz = sh[40 + zz];
+                      if (oz >= 0) {
+                        unsigned& oe = ckMap[ck_map_idx(oz >> 16, oz & 0xffff)];
+                        if ((oe & 15) == (unsigned)zz && (int)(oe >> 4) == oz)
+                          __hip_atomic_store(&oe, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                      }
+                      sh[40 + zz] = key;
+                      sh[48 + zz] = 1;
+                    }
+                  }
+                  __hip_atomic_store(&sh[36], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                zz = uni(__shfl(zz, 0, 64));
+                if (zz >= 0) {
+                  recompute_chunk<R>(F, P, reqS, reqB0, win + (size_t)zz * kSlotDw, ckArea, lane);
+                  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                  if (lane == 0) {
+                    __hip_atomic_store(&ckMap[ck_map_idx(reqS, reqB0)],
+                                       ((unsigned)reqS << 20) | ((unsigned)reqB0 << 4) | (unsigned)zz,
+                                       __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(&sh[48 + zz], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                  }
+                  ++nSelf;
+                  continue;                                // re-check the map
+                }
+              }
+              if (it > (1 << 26)) break;
               __builtin_amdgcn_s_sleep(1);
             }
-            if (it > (1 << 22)) { status = 5; done = 1; break; }   // 5: BG_INTERNAL
+            if (!got) { status = 5; done = 1; break; }     // 5: BG_INTERNAL (unreachable)
             k0 = -1000000;                                 // decode the neighbourhood again
             ++nMiss;
             if (F.dbg) tMiss += __builtin_readcyclecounter() - tw0;
@@ -785,6 +833,15 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     ++nMiss;
     reqS = uni(sh[4]);
     reqB0 = uni(sh[5]);
+    // the chunk (window) just loaded for this request always holds the requested cell, so a
+    // repeated request is a defect: end the walk with BG_INTERNAL rather than loop forever
+    sameReq = (reqS == lastReqS && reqB0 == lastReqB) ? sameReq + 1 : 0;
+    lastReqS = reqS;
+    lastReqB = reqB0;
+    if (sameReq > 2) {
+      if (tid == 0) sh[9] = 5;
+      break;
+    }
     if constexpr (CK) {
       // recompute the requested chunk and up to three chunks to its left (the walk heads up and
       // left), one per wave, into the oldest slots
@@ -865,11 +922,11 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     u64* d = F.dbg + (size_t)P.index * 8;
     d[0] = __builtin_readcyclecounter() - tWalk0;
     d[1] = tJump + tDec; d[2] = nJump + nDec; d[3] = tMiss; d[4] = nMiss; d[5] = (u64)ncore;
-    d[6] = async ? (u64)sh[37] : nRec;
+    d[6] = async ? (u64)sh[37] + nSelf : nRec;
   }
 
   // ---------------- semiglobal prefix gaps (:416-428); every wave knows k, l through sh
-  if (wid == 0 && lane == 0) { sh[7] = k; sh[8] = l; sh[9] = status; sh[10] = ncore; }
+  if (wid == 0 && lane == 0) { sh[7] = k; sh[8] = l; sh[10] = ncore; if (sh[9] != 5) sh[9] = status; }
   __syncthreads();
   const int kstop = sh[7], lstop = sh[8];
   status = sh[9];

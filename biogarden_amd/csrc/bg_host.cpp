@@ -130,6 +130,14 @@ struct bg_aligner {
   std::vector<BgResult> hres;
   std::vector<uint8_t> ho1, ho2;
 
+  // The reference aligner's scratch dims (aligner.rs:30 buffer_size): 1024 x 1024 at
+  // SequenceAligner::new (:44-55), reset to (len1+1, len2+1) by a call with len1 > rows ||
+  // len2 > cols (:92-94, 594-602).  A prepared batch is that many calls in caller order;
+  // bufAt[p] is the state pair p's call starts from (what bg_ref_divergent judges it against).
+  long bufRows = 1024, bufCols = 1024;
+  std::vector<std::pair<long, long>> bufAt;
+  int finWaves = 0, finSlots = 0;   // last prepared batch: finish workgroup geometry
+
   size_t device_bytes() const {
     size_t t = seq1.cap + seq2.cap + codes1.cap + codes2.cap + lut.cap + prof.cap + pairs.cap + recs.cap;
     for (const Slot& S : slot)
@@ -552,6 +560,19 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     for (int c = 0; c < 32; ++c) present[c] |= loc[c];
   }
 
+  // ---- the reference's scratch history over the batch's calls (aligner.rs:92-94): the
+  // argument errors return before the resize, everything else (the score panic included)
+  // resizes first.  Edit distance and LCS do not use a SequenceAligner.
+  long bufR = h->bufRows, bufC = h->bufCols;
+  h->bufAt.assign(npairs, std::make_pair(bufR, bufC));
+  for (size_t p = 0; p < npairs; ++p) {
+    h->bufAt[p] = std::make_pair(bufR, bufC);
+    if (h->finFlags || h->prestatus[p] == BG_INVALID_ARGUMENT_RANGE ||
+        h->prestatus[p] == BG_INVALID_INPUT_SIZE)
+      continue;
+    if ((long)n1[p] > bufR || (long)n2[p] > bufC) { bufR = (long)n1[p] + 1; bufC = (long)n2[p] + 1; }
+  }
+
   // ---- dense alphabet, profile, kernel family
   int dense[32];
   int K = 0;
@@ -595,7 +616,9 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
         if (v - 3 < -128 || v - 2 > 127) tagOK = false;
       }
   h->tag = tagOK ? 1 : 0;
-  h->ckpt = (h->tag && h->allowCkpt) ? 1 : 0;
+  bool ckLimit = false;   // a pair beyond the checkpoint tracebacks' chunk keys (BG_CK_MAX_*)
+plan_again:
+  h->ckpt = (h->tag && h->allowCkpt && !ckLimit) ? 1 : 0;
   // affine / local score-only kernel (bg_aff_common.h): int8 profile entries S - 2a (local
   // S - a); values, and the finite -inf drifting by e = b - a per step, far from wrapping
   bool ackOK = !h->tag && h->allowAck && bound < 268435456.0 &&
@@ -606,7 +629,7 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
         const int64_t v = (int64_t)sc->table[q * 32 + c] - (mode == BG_LOCAL ? 1 : 2) * (int64_t)a;
         if (v < -128 || v > 127) ackOK = false;
       }
-  h->ack = ackOK ? 1 : 0;
+  h->ack = (ackOK && !ckLimit) ? 1 : 0;
 
   // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair, or a group
   // of workgroups per pair in the tagged kernel's WIDE mode)
@@ -614,6 +637,11 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   h->wide = 0;
   if (h->tag && plan_wide(h, n1, n2, npairs, &R, &W)) h->wide = 1;
   else plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
+  if ((h->ckpt || h->ack) && ncomp &&
+      ((maxn1 + 64 * R - 1) / (64 * R) >= BG_CK_MAX_STRIPS || maxn2 / 64 + 2 >= BG_CK_MAX_CHUNKS)) {
+    ckLimit = true;
+    goto plan_again;
+  }
   size_t lds = 0;
   if (h->tag) {
     // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
@@ -706,6 +734,8 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     oo += n1[p] + n2[p];
     P.wg_count = h->wide ? std::max(1, h->groupOf[p]) : 1;
     P.prog_off = h->wide ? h->progWords : 0;
+    P.buf_rows = (int32_t)std::min<long>(h->bufAt[p].first, 0x7FFFFFFF);
+    P.buf_cols = (int32_t)std::min<long>(h->bufAt[p].second, 0x7FFFFFFF);
     if (h->wide) {
       for (int g = 0; g < P.wg_count; ++g) h->wgmap.push_back(make_int2((int)h->plan.size(), g));
       h->progWords += (uint32_t)(P.wg_count * W);
@@ -817,6 +847,9 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   }
   BG_HIP(hipStreamSynchronize(h->stream));
   h->order_ = order;
+  h->bufRows = bufR;
+  h->bufCols = bufC;
+  fin_geom(h, h->plan.size(), &h->finWaves, &h->finSlots);
   h->prepared = true;
   return BG_OK;
 }
@@ -899,6 +932,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.area_ints = 0;
     F.flags = h->finFlags;
     if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;
+    if (std::getenv("BG_FIN_SELFSERVE")) F.flags |= BG_FIN_SELFSERVE;
     if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(64 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, h->stream2));
@@ -1008,7 +1042,8 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
     if (r.out_len > (uint32_t)(P.n1 + P.n2) || r.out_start + r.out_len > (uint32_t)(P.n1 + P.n2)) return BG_E_HIP;
     std::memcpy(out1 + h->outoff[p], h->ho1.data() + P.out_off + r.out_start, r.out_len);
     std::memcpy(out2 + h->outoff[p], h->ho2.data() + P.out_off + r.out_start, r.out_len);
-    if (o.status == BG_OK && bg_ref_fresh_divergent(h->mode, (long)h->n1v[p], (long)h->n2v[p], r.score))
+    if (o.status == BG_OK && bg_ref_divergent(h->mode, (long)h->n1v[p], (long)h->n2v[p], r.score,
+                                              h->bufAt[p].first, h->bufAt[p].second))
       o.status = BG_REF_DIVERGENT;
   }
   return BG_OK;
@@ -1059,6 +1094,15 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->npairs = (int32_t)h->npairs;
   o->dp_ms = h->dp_ms;
   o->finish_ms = h->fin_ms;
+  o->fin_waves = h->finWaves;
+  o->fin_slots = h->finSlots;
+  return BG_OK;
+}
+
+extern "C" int bg_aligner_buffer_size(bg_aligner* h, size_t* rows, size_t* cols) {
+  if (!h || !rows || !cols) return BG_E_ARG;
+  *rows = (size_t)h->bufRows;
+  *cols = (size_t)h->bufCols;
   return BG_OK;
 }
 

@@ -402,7 +402,7 @@ __global__ __launch_bounds__(256) void bg_export_kernel(BgExportArgs E) {
   if (threadIdx.x == 0) {
     BgPairResultDev o;
     o.status = r.status;
-    if (o.status == 0 && bg_ref_fresh_divergent(E.mode, P.n1, P.n2, r.score)) o.status = 4;
+    if (o.status == 0 && bg_ref_divergent(E.mode, P.n1, P.n2, r.score, P.buf_rows, P.buf_cols)) o.status = 4;
     o.score = r.score;
     o.offset = P.caller_off;
     o.len = r.out_len;

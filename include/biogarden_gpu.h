@@ -101,7 +101,11 @@ typedef struct bg_pair_result {
 } bg_pair_result;
 
 /* Many independent pairs with one mode / scoring / (a, b) — the batched form of one
- * SequenceAligner::*_alignment call.  out1/out2 capacity >= sum(n1+n2).  Returns 0 or BG_E_*. */
+ * SequenceAligner::*_alignment call per pair, in order, on one aligner.  out1/out2 capacity
+ * >= sum(n1+n2).  Returns 0 or BG_E_*.
+ * Sizes: each length <= 2^30 - 1 (BG_E_ARG beyond).  Pairs too long for the checkpoint
+ * tracebacks' chunk keys (>= 4096 strips of 64R rows, or len2 >= ~4.19M) run the full-trace
+ * kernels instead (BG_E_NOMEM if that trace does not fit the device). */
 int bg_align_batch(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
                    const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                    const bg_scoring* scoring, int32_t a, int32_t b, bg_pair_result* results,
@@ -137,9 +141,18 @@ typedef struct bg_stats {
   int32_t checkpoint;      /* 1: score-only DP + traceback recomputing the chunks its path crosses */
   float dp_ms;             /* last execute: DP kernel time (HIP events on the handle's stream) */
   float finish_ms;         /* last execute: end-cell + traceback kernel time */
+  int32_t fin_waves;       /* finish workgroup: waves (walker + recomputing helpers) */
+  int32_t fin_slots;       /* finish workgroup: recomputed-chunk slots in use (0: all) */
 } bg_stats;
 
 int bg_get_stats(bg_aligner* h, bg_stats* out);
+
+/* The reference aligner's scratch dims this handle models (SequenceAligner::buffer_size,
+ * aligner.rs:30): 1024 x 1024 after bg_aligner_new (:44-55); every alignment call of a prepared
+ * batch, in caller order, resizes it to (len1+1, len2+1) when len1 > rows || len2 > cols
+ * (:92-94, 594-602), as the reference's calls would.  Status BG_REF_DIVERGENT is judged against
+ * the dims each call starts from. */
+int bg_aligner_buffer_size(bg_aligner* h, size_t* rows, size_t* cols);
 
 /* Kernel timing over a region of executes (HIP events recorded on the handle's stream around
  * the DP and the finish kernel of every execute; up to 4096 executes per region).

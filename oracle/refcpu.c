@@ -85,6 +85,16 @@ or_aligner* or_aligner_new(void) {
   return A;
 }
 
+/* A reference aligner whose scratch is rows x cols (as after resize_buffers(rows, cols),
+ * aligner.rs:594-602): the state a reused SequenceAligner reaches; tests mirror a product
+ * handle's modelled history with it. */
+or_aligner* or_aligner_new_dims(size_t rows, size_t cols) {
+  or_aligner* A = (or_aligner*)calloc(1, sizeof(or_aligner));
+  if (!A) return NULL;
+  if (alloc_buffers(A, rows, cols)) { free_buffers(A); free(A); return NULL; }
+  return A;
+}
+
 or_aligner* or_aligner_new_exact(void) {
   or_aligner* A = or_aligner_new();
   if (A) A->exact = 1;

@@ -53,6 +53,7 @@ typedef struct or_aligner or_aligner;
 
 or_aligner* or_aligner_new(void);        /* reference SequenceAligner::new()  */
 or_aligner* or_aligner_new_exact(void);  /* product semantics: exact-size buffers per call */
+or_aligner* or_aligner_new_dims(size_t rows, size_t cols);  /* reference aligner after a resize */
 void or_aligner_free(or_aligner* A);
 void or_buffer_size(const or_aligner* A, size_t* rows, size_t* cols);
 

@@ -34,6 +34,8 @@ def lib():
         L = ctypes.CDLL(path)
         L.or_aligner_new.restype = ctypes.c_void_p
         L.or_aligner_new_exact.restype = ctypes.c_void_p
+        L.or_aligner_new_dims.restype = ctypes.c_void_p
+        L.or_aligner_new_dims.argtypes = [ctypes.c_size_t, ctypes.c_size_t]
         L.or_aligner_free.argtypes = [ctypes.c_void_p]
         L.or_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
                                      ctypes.POINTER(ctypes.c_size_t)]
@@ -82,9 +84,12 @@ def scoring(name_or_table):
 class Aligner:
     """Reference-faithful SequenceAligner (exact=False) or exact-size product semantics."""
 
-    def __init__(self, exact=False):
+    def __init__(self, exact=False, dims=None):
         L = lib()
-        self._p = L.or_aligner_new_exact() if exact else L.or_aligner_new()
+        if dims is not None:
+            self._p = L.or_aligner_new_dims(dims[0], dims[1])
+        else:
+            self._p = L.or_aligner_new_exact() if exact else L.or_aligner_new()
 
     def __del__(self):
         if getattr(self, "_p", None):

@@ -18,63 +18,17 @@ from conftest import REF_FIX, REFERENCE_DOCTESTS, REFERENCE_GOLDENS, read_fasta
 
 pytestmark = pytest.mark.gpu
 
-DNA = b"ACGT"
-PROT = b"ACDEFGHIKLMNPQRSTVWY"
+from parity_util import DNA, PROT, check_batch, mutate, rand_seq, rescore_semiglobal
 
 
-@pytest.fixture(scope="module")
+@pytest.fixture
 def aligner():
+    """A new SequenceAligner per test (the reference's tests each start from
+    SequenceAligner::new(), whose 1024 x 1024 scratch the divergence flags depend on)."""
     from biogarden_amd.alignment.aligner import SequenceAligner
     al = SequenceAligner(0)
     yield al
     al.close()
-
-
-def rand_seq(rng, n, alpha):
-    return bytes(rng.choice(alpha) for _ in range(n))
-
-
-def mutate(rng, s, alpha, rate=0.1):
-    out = bytearray()
-    for ch in s:
-        r = rng.random()
-        if r < rate / 3:
-            continue                                   # deletion
-        if r < 2 * rate / 3:
-            out.append(rng.choice(alpha))              # insertion
-        out.append(rng.choice(alpha) if rng.random() < rate / 3 else ch)
-    return bytes(out)
-
-
-def check_batch(aligner, oracle, mode, pairs, scoring, a, b, fresh=True):
-    from biogarden_amd.alignment import score as score_mod
-    res = aligner.align_batch(mode, pairs, getattr(score_mod, scoring), a, b)
-    bad = []
-    for (s1, s2), r in zip(pairs, res):
-        st, sc, o1, o2 = oracle.align(mode, s1, s2, scoring, a, b, exact=True)
-        got = (r.status, r[0], bytes(r[1].chain), bytes(r[2].chain))
-        if st == 0 and r.status in (0, 4) and got[1:] == (sc, o1, o2):
-            pass                                     # same answer (4 = fresh reference differs)
-        elif st in (4, 5) and r.status == 4:
-            pass                                     # the reference panics: flagged
-        elif st == r.status and st in (1, 2, 3):
-            pass
-        else:
-            bad.append((len(s1), len(s2), s1[:40], s2[:40], (st, sc), got[:2]))
-        if fresh:
-            fst, fsc, f1, f2 = oracle.align(mode, s1, s2, scoring, a, b, exact=False)
-            if fst == 0 and st == 0 and (fsc, f1, f2) != (sc, o1, o2):
-                # the fresh reference answers from stale scratch beyond the pair (history
-                # dependent, A.7): we return the exact-size answer and flag it
-                if r.status != 4:
-                    bad.append(("stale-not-flagged", len(s1), len(s2), r.status))
-            elif fst == 0:
-                if not (r.status == 0 and (r[0], bytes(r[1].chain), bytes(r[2].chain)) == (fsc, f1, f2)):
-                    bad.append(("fresh-ok", len(s1), len(s2), fst, r.status, fsc, r[0]))
-            elif r.status == 0:
-                bad.append(("fresh-panics-but-ok", len(s1), len(s2), fst, s1[:30], s2[:30]))
-    assert not bad, bad[:5]
-    return res
 
 
 # ------------------------------------------------------------------ reference goldens
@@ -291,28 +245,6 @@ def test_unscorable_and_empty(aligner, oracle):
 
 
 # ------------------------------------------------------------------ BASELINE-size properties
-
-
-def rescore_semiglobal(r, s1, s2, table, a):
-    """Score of the emitted alignment under the linear model (a >= b): end gaps
-    free, every other gap column costs a."""
-    n1, n2 = len(s1), len(s2)
-    ei, ej = r.end
-    k0, l0 = r.start
-    colcase = ei < n1
-    a1, a2 = bytes(r[1].chain), bytes(r[2].chain)
-    tail = (n1 - ei) if colcase else (n2 - ej)
-    pre = k0 if colcase else l0
-    core1, core2 = a1[pre:len(a1) - tail], a2[pre:len(a2) - tail]
-    sc = 0
-    for x, y in zip(core1, core2):
-        if x == 45 or y == 45:
-            sc += a
-        else:
-            sc += table[x - 65][y - 65]
-    degap1 = a1.replace(b"-", b"")
-    degap2 = a2.replace(b"-", b"")
-    return sc, degap1, degap2
 
 
 def test_baseline_size_semiglobal_properties(aligner, oracle):

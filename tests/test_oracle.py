@@ -122,3 +122,33 @@ def test_scs_merge_matches_oracle(oracle):
         b = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(0, 40)))
         lcs = oracle.longest_common_subsequence(a, b)
         assert _merge(a, b, lcs) == oracle.shortest_common_supersequence(a, b)
+
+
+def test_C1_derived_golden_reproduced(oracle):
+    """The committed C1 golden (oracle-derived, tools/make_derived_goldens.py) is what the
+    reference-faithful oracle computes for examples/from_file.rs's call."""
+    with open(os.path.join(GOLDEN, "derived", "C1_semiglobal_blosum62_o1_e2.json")) as f:
+        gold = json.load(f)
+    assert gold["derived"] is True
+    inp = read_fasta(os.path.join(REF_FIX, "input", "semiglobal_alignment.fasta"))
+    assert (len(inp[0][1]), len(inp[1][1])) == (gold["len1"], gold["len2"]) == (9559, 8457)
+    st, score, a1, a2 = oracle.align("semiglobal", inp[0][1], inp[1][1], "blosum62", -1, -2)
+    assert (st, score, a1, a2) == (0, gold["score"], gold["aligned1"].encode(), gold["aligned2"].encode())
+
+
+def test_reused_aligner_scratch_model(oracle):
+    """resize_buffers only on a strict overflow, both dims reset (aligner.rs:92-94, 594-602):
+    a length equal to the current dim panics, one beyond it resizes; errors return first."""
+    al = oracle.Aligner()
+    assert al.buffer_size() == (1024, 1024)
+    assert al.align("global", b"A" * 2000, b"C" * 10, "unit", -1, -1)[0] == 0
+    assert al.buffer_size() == (2001, 11)
+    assert al.align("global", b"A" * 1024, b"C" * 11, "unit", -1, -1)[0] == 4   # col 11 == dim
+    assert al.buffer_size() == (2001, 11)
+    assert al.align("global", b"A" * 1024, b"C" * 12, "unit", -1, -1)[0] == 0   # 12 > 11: resize
+    assert al.buffer_size() == (1025, 13)
+    assert al.align("global", b"A" * 5000, b"C", "unit", 1, -1)[0] == 1         # error, no resize
+    assert al.buffer_size() == (1025, 13)
+    d = oracle.Aligner(dims=(1025, 13))
+    assert d.buffer_size() == (1025, 13)
+    assert d.align("global", b"A" * 1025, b"C", "unit", -1, -1)[0] == 4
