@@ -411,14 +411,17 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
                          : h->ckpt ? 2 * Rc + 2 : (h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12));
     const int S = maxn1 ? (int)((maxn1 + 64 * Rc - 1) / (64 * Rc)) : 1;
     // many pairs on the affine / local checkpoint path: at most 4 waves per pair (C5: R = 2 runs
-    // W = 4 at 2 232 GCUPS, W = 8 at 2 077; every CU holds several pairs anyway)
-    const int wmax = (!h->ack && (h->affine || h->local)) ? 8 : ((h->ack && np >= (size_t)h->cus) ? 4 : 16);
+    // W = 4 at 2 232 GCUPS, W = 8 at 2 077; every CU holds several pairs anyway).  With fewer
+    // than two pairs per CU a 4-wave workgroup leaves one wave per SIMD and the step's dependent
+    // chain unhidden (MA, 256 x 10k x 10k -11/-1: R = 2 / W = 4 DP 13.3 ms, R = 8 / W = 8 5.9 ms)
+    const bool manyAck = h->ack && np >= 2 * (size_t)h->cus;
+    const int wmax = h->tuneW ? 16 : (!h->ack && (h->affine || h->local)) ? 8 : (manyAck ? 4 : 16);
     for (int Wc = 1; Wc <= wmax; ++Wc) {
       if (h->tuneW && Wc != h->tuneW) continue;
       if (Wc > S && !h->tuneW) continue;
       // many pairs on the affine / local path: wave counts that divide over the 4 SIMDs (W = 3
       // estimates best for C5 and measures worst: 2 089 GCUPS against 2 232 at R = 2 / W = 4)
-      if (h->ack && np >= (size_t)h->cus && !h->tuneW && (Wc & (Wc - 1))) continue;
+      if (manyAck && !h->tuneW && (Wc & (Wc - 1))) continue;
       const int wps = (Wc + 3) / 4;                      // waves per SIMD per workgroup
       const int want = (int)((np + h->cus - 1) / h->cus);
       int wg = std::min(want, 32 / Wc);
@@ -469,7 +472,10 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
         const int a = std::max(1, (A * wg + 3) / 4);
         T += 64.0 * opsPerStep * a * (4.0 + 3.0 / a);
       }
-      const double rounds = std::ceil((double)np / ((double)h->cus * wg));
+      // workgroups are dealt dynamically, so a partial last round costs its share, not a full
+      // round (C4, 32 pairs per CU: R = 3 at 28 resident runs 1.14 rounds, 1.80 ms, against
+      // R = 5 at 16 resident, 2 rounds, 2.32 ms; a whole-round count picked R = 5)
+      const double rounds = std::max(1.0, (double)np / ((double)h->cus * wg));
       T *= rounds;
       if (h->ack) {
         // the traceback recomputes the chunks its path crosses: per pair ~ (600 + 8R^2) cycles
@@ -477,7 +483,11 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
         // flight per CU as the finish workgroup's LDS allows
         const double fwg = std::max(1.0, std::floor(160.0 * 1024 / (double)std::max<size_t>(finLds, 1)));
         const double frounds = std::ceil((double)np / ((double)h->cus * fwg));
-        T += frounds * (600.0 + kFinR2 * Rc * Rc) * (double)(maxn1 + maxn2) * 0.5;
+        const double Tf = frounds * (600.0 + kFinR2 * Rc * Rc) * (double)(maxn1 + maxn2) * 0.5;
+        // pipelined (depth > 1): the traceback of step k runs beside the DP of step k + 1; the
+        // step is the longer of the two plus ~0.2 of the shorter (interference), as measured
+        // on MA across R = 2..8, W = 4..16 (tools/aff_sweep.sh)
+        T = (h->depth > 1 && !manyAck) ? std::max(T, Tf) + 0.2 * std::min(T, Tf) : T + Tf;
       }
       const int wpsAll = wps * wg;
       cands.push_back({T, Rc, Wc, wpsAll, rowc ? 1 : 0});
