@@ -99,6 +99,8 @@ struct BgDpArgs {
   int32_t aux_lds_off;     // tagged kernel: per-wave area (boundary block, ring, profile, codes)
   const int2* wgmap;       // tagged kernel, WIDE mode: per workgroup (plan index, index in group)
   uint32_t* gprog;         // tagged kernel, WIDE mode: global per-wave progress counters
+  unsigned long long* dbg; // optional per-wave timestamps of the first strip (env BG_DP_TIMING):
+                           // [gw * 8 + k], k: 0 strip, 1 start, 2 chunk 0 done, 3 end, 4 waited
 };
 
 struct BgFinishArgs {

@@ -121,7 +121,7 @@ struct bg_aligner {
   std::vector<int2> wgmap;
   int gridWgs = 0;
   uint32_t progWords = 0;
-  DevBuf wgmapBuf, gprogBuf, dbgBuf;
+  DevBuf wgmapBuf, gprogBuf, dbgBuf, dpDbg;
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
   float dp_ms = 0.f, fin_ms = 0.f;
@@ -297,7 +297,8 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
   size_t maxn1 = 0;
   for (size_t p : comp) maxn1 = std::max(maxn1, n1[p]);
   if (maxn1 < 64 * 4 * 16) return false;                   // one workgroup's 16 waves suffice
-  const int W = 4;
+  int W = 4;
+  if (const char* e = std::getenv("BG_WIDE_W")) W = std::max(1, std::min(16, std::atoi(e)));
   const int cand[] = {2, 3, 4, 5, 8, 10};
   double best = 1e300;
   int bestR = 0;
@@ -895,6 +896,11 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.aux_lds_off = h->auxLdsOff;
     A.wgmap = h->wgmapBuf.as<int2>();
     A.gprog = h->gprogBuf.as<uint32_t>();
+    A.dbg = nullptr;
+    if (std::getenv("BG_DP_TIMING") && h->tag && h->dpDbg.ensure(64 * 4096)) {
+      A.dbg = h->dpDbg.as<unsigned long long>();
+      BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, h->stream));
+    }
     if (h->wide) BG_HIP(hipMemsetAsync(h->gprogBuf.p, 0, 4 * (size_t)h->progWords, h->stream));
     A.trace = S.trace.as<uint32_t>();
     A.bndM = S.bndM.as<int32_t>();
@@ -1011,6 +1017,24 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   int rc = bg_synchronize(h);
   if (rc) return rc;
   const size_t np = h->plan.size();
+  if (std::getenv("BG_DP_TIMING") && h->dpDbg.p && np) {
+    // first pair's waves: strip start / chunk-0 end / strip end relative to the earliest start
+    // (s_memrealtime, 100 MHz, one clock for every XCD), and the shader cycles each wave spent
+    // polling for the strip above out of its whole strip (s_memtime)
+    std::vector<unsigned long long> d(8 * 4096);
+    BG_HIP(hipMemcpy(d.data(), h->dpDbg.p, 64 * 4096, hipMemcpyDeviceToHost));
+    unsigned long long t0 = ~0ull, tend = 0;
+    for (int g = 0; g < 4096; ++g)
+      if (d[8 * g + 1]) { t0 = std::min(t0, d[8 * g + 1]); tend = std::max(tend, d[8 * g + 3]); }
+    std::fprintf(stderr, "dp timing: span %.1f us\n", (tend - t0) * 0.01);
+    for (int g = 0; g < 4096; ++g) {
+      if (!d[8 * g + 1]) continue;
+      if (g % 16 && g + 1 < 4096 && d[8 * (g + 1) + 1]) continue;   // every 16th wave + the last
+      std::fprintf(stderr, "  wave %4d strip %4llu start %8.1f c0done %8.1f end %8.1f us  waited %10.0f of %10.0f cycles\n", g,
+                   d[8 * g], (d[8 * g + 1] - t0) * 0.01, (d[8 * g + 2] - t0) * 0.01,
+                   (d[8 * g + 3] - t0) * 0.01, (double)d[8 * g + 4], (double)d[8 * g + 5]);
+    }
+  }
   if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.p && np) {
     std::vector<unsigned long long> d(8 * np);
     BG_HIP(hipMemcpy(d.data(), h->dbgBuf.p, 64 * np, hipMemcpyDeviceToHost));

@@ -199,7 +199,28 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
                            : nullptr;
     int cv[3] = {0, 0, 0};
     if (!rowInLds) fetch_codes(0, cv);
+    // WIDE, strip above on another workgroup: its blocks come through HBM one chunk ahead of
+    // use — block c + 1 (and the producer's counter for the check at chunk c + 1) is loaded
+    // while chunk c computes, so neither the counter poll nor the block load (each a cross-XCD
+    // L2 / MALL round trip of ~1-2 us) sits between two chunks of the strip pipeline
+    const bool hbmAhead = WIDE && s > 0 && !mailIn;
+    const int pwH = (s - 1) % GW;
+    const int needBase = ((s - 1) / GW) * nblk;
+    const int32_t* bndAbove = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + lane;
+    int nbV = 0, pollV = 0;
+    if (hbmAhead) {
+      if (0 < nblk)
+        while ((int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < needBase + 1)
+          __builtin_amdgcn_s_sleep(2);
+      nbV = load_agent(bndAbove);
+      pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const bool dbgOn = A.dbg != nullptr && rho == 0 && pairIdx == 0 && gw < 4096;
+    unsigned long long tWait = 0, tStart = dbgOn ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long cStart = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
     for (int c = 0; c < NC; ++c) {
+      if (dbgOn && c == 1 && lane == 0) A.dbg[gw * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long tw0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
       if (rowInLds) {
         C.codeLane = sRow + c * BG_CHUNK - lane - 1;
       } else {
@@ -214,6 +235,19 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         const int m0 = wadd(row0_M(mode, jb, a, b), -wmul(a, jb));          // M'(0, j)
         waveLds[lane] = CKPT ? m0 : 4 * m0 + 2;                             // (X form)
         C.bIn = waveLds;
+      } else if (hbmAhead) {
+        waveLds[lane] = nbV;                                                // block c
+        C.bIn = waveLds;
+        if (c + 1 < NC) {
+          if (c + 1 < nblk) {
+            while (pollV < needBase + c + 2) {
+              __builtin_amdgcn_s_sleep(2);
+              pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+          nbV = load_agent(bndAbove + (size_t)(c + 1) * BG_CHUNK);         // block c + 1
+          pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
       } else {
         if (c < nblk) {
           const int need = ((s - 1) / GW) * nblk + c + 1;
@@ -242,6 +276,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
           __builtin_amdgcn_s_sleep(1);
         C.mail = mailbox + ((seq - 1) % kMailSlots) * 64;
       }
+      if (dbgOn) tWait += __builtin_amdgcn_s_memtime() - tw0;
       const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
       if constexpr (CKPT) {
         int32_t* ck = ckBase + (size_t)c * (R + 1) * BG_WAVE;
@@ -293,6 +328,13 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       }
       if (mailIn && lane == 0)   // release: this chunk's reads of the slot are done
         __hip_atomic_store(sCons + w, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (dbgOn && lane == 0) {
+      A.dbg[gw * 8 + 0] = (unsigned long long)s;
+      A.dbg[gw * 8 + 1] = tStart;
+      A.dbg[gw * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+      A.dbg[gw * 8 + 4] = tWait;
+      A.dbg[gw * 8 + 5] = __builtin_amdgcn_s_memtime() - cStart;
     }
   }
 }
