@@ -55,6 +55,79 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+def _oracle_results(pairs, mode, a, b):
+    """What a rank's bg_batch_fetch returns for its shard, computed by the CPU oracle (the GPU
+    path is bit-exact with it, tests/test_gpu_*.py): status, score and both aligned strings."""
+    from oracle import refcpu
+    out = []
+    for s1, s2 in pairs:
+        st, sc, o1, o2 = refcpu.align(mode, s1, s2, "blosum62", a, b, exact=True)
+        out.append({"status": st, "score": sc, "aligned1": o1, "aligned2": o2,
+                    "end": (len(s1), len(s2)), "start": (0, 0)})
+    return out
+
+
+def _real_pairs(n, seed):
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        s1 = bytes(rng.choice(b"ACGT") for _ in range(rng.randint(0, 300)))
+        s2 = bytearray(s1[rng.randint(0, len(s1)):] if s1 else b"")
+        for k in range(len(s2)):
+            if rng.random() < 0.1:
+                s2[k] = rng.choice(b"ACGT")
+        s2 = bytes(s2) + bytes(rng.choice(b"ACGT") for _ in range(rng.randint(0, 60)))
+        out.append((s1, s2))
+    return out
+
+
+def _sharded_worker(rank, world, port, q, mode, a, b):
+    """One rank of a sharded batch: LPT shard -> align its pairs -> pack them in
+    bg_batch_export's record layout -> variable-size gather to rank 0 -> decode + merge in
+    the caller's pair order."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        pairs = _real_pairs(37, 11)
+        shards = shard.lpt_shards([(len(x), len(y)) for x, y in pairs], world)
+        mine = _oracle_results([pairs[p] for p in shards[rank]], mode, a, b)
+        local = torch.frombuffer(bytearray(shard.encode_export(mine)), dtype=torch.uint8)
+        got = shard.gather_packed(local, dist, dst=0)
+        if rank == 0:
+            merged = shard.merge_shards(shards, [_native.decode_export(x) for x in got])
+            single = _oracle_results(pairs, mode, a, b)
+            q.put(("ok", merged == single, len(merged), [len(s) for s in shards]))
+        else:
+            q.put(("rank", rank, got is None))
+    except Exception as e:  # surface worker failures to the test
+        q.put(("err", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_batch_equals_single_rank(world):
+    """The multi-rank data path on CPU ranks: the merged gather of every rank's packed shard
+    equals a single-rank run of the same pairs, pair for pair (status, score, both strings)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, "semiglobal", -11, -1))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+    ok = [m for m in msgs if m[0] == "ok"]
+    assert len(ok) == 1, msgs
+    assert ok[0][1] and ok[0][2] == 37 and min(ok[0][3]) > 0, ok
+    assert all(m[0] in ("ok", "rank") for m in msgs), msgs
+    assert all(p.exitcode == 0 for p in procs)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
