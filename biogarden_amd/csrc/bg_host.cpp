@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <numeric>
+#include <thread>
 #include <vector>
 
 #include "bg_device.h"
@@ -62,7 +63,62 @@ struct DevBuf {
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Pinned host staging (hipHostMalloc): uploads and downloads DMA straight from / into it, with
+// no runtime bounce copy; grown and kept by the handle like its device arenas.
+struct PinBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) { p = nullptr; return false; }
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
 inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
+
+// Host worker threads for the byte passes of prepare / fetch: at most 16 (a GPU's share of the
+// host's cores on the MI355X nodes), one per ~1 MiB of input, BG_HOST_THREADS overrides.
+int host_threads(uint64_t bytes) {
+  int t = 16;
+  if (const char* e = std::getenv("BG_HOST_THREADS")) t = std::max(1, std::atoi(e));
+  const unsigned hw = std::thread::hardware_concurrency();
+  if (hw) t = std::min<int>(t, (int)hw);
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)t, bytes / (1 << 20) + 1));
+}
+
+// Runs fn(lo, hi) over [0, n) split into contiguous ranges of about equal weight
+// (weight(i) = bytes of item i), one per thread; inline when one thread suffices.
+template <class Wt, class F>
+void par_ranges(size_t n, Wt weight, F fn) {
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += weight(i);
+  const int T = host_threads(total);
+  if (T <= 1 || n < 2) { fn((size_t)0, n); return; }
+  std::vector<std::thread> th;
+  size_t lo = 0;
+  uint64_t acc = 0;
+  for (int k = 0; k < T && lo < n; ++k) {
+    const uint64_t goal = total * (uint64_t)(k + 1) / (uint64_t)T;
+    size_t hi = lo;
+    while (hi < n && (acc < goal || hi == lo)) acc += weight(hi++);
+    if (k == T - 1) hi = n;
+    th.emplace_back(fn, lo, hi);
+    lo = hi;
+  }
+  for (auto& x : th) x.join();
+}
 
 }  // namespace
 
@@ -128,7 +184,9 @@ struct bg_aligner {
   hipEvent_t last[4] = {nullptr, nullptr, nullptr, nullptr};
 
   std::vector<BgResult> hres;
-  std::vector<uint8_t> ho1, ho2;
+  PinBuf ho1, ho2;                 // fetch: the slot's aligned strings, downloaded
+  PinBuf up;                       // prepare: raw residues + codes of the batch, uploaded
+  std::vector<uint32_t> pmask;     // prepare: per pair, the score codes its residues use
 
   // The reference aligner's scratch dims (aligner.rs:30 buffer_size): 1024 x 1024 at
   // SequenceAligner::new (:44-55), reset to (len1+1, len2+1) by a call with len1 > rows ||
@@ -217,7 +275,8 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs,
-                    &h->wgmapBuf, &h->gprogBuf}) d->release();
+                    &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg}) d->release();
+  for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
   for (Slot& S : h->slot) {
     for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results}) d->release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
@@ -416,7 +475,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
     // than two pairs per CU a 4-wave workgroup leaves one wave per SIMD and the step's dependent
     // chain unhidden (MA, 256 x 10k x 10k -11/-1: R = 2 / W = 4 DP 13.3 ms, R = 8 / W = 8 5.9 ms)
     const bool manyAck = h->ack && np >= 2 * (size_t)h->cus;
-    const int wmax = h->tuneW ? 16 : (!h->ack && (h->affine || h->local)) ? 8 : (manyAck ? 4 : 16);
+    const int wmax = (!h->ack && (h->affine || h->local)) ? 8 : ((manyAck && !h->tuneW) ? 4 : 16);
     for (int Wc = 1; Wc <= wmax; ++Wc) {
       if (h->tuneW && Wc != h->tuneW) continue;
       if (Wc > S && !h->tuneW) continue;
@@ -556,20 +615,41 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     if (n1[p] > 0x3FFFFFFF || n2[p] > 0x3FFFFFFF) return BG_E_ARG;
     if (needNonPos && (a > 0 || b > 0)) { h->prestatus[p] = BG_INVALID_ARGUMENT_RANGE; continue; }
     if (mode == BG_FITTING && n1[p] < n2[p]) { h->prestatus[p] = BG_INVALID_INPUT_SIZE; continue; }
-    if (n1[p] == 0 || n2[p] == 0) continue;           // the score closure is never called
-    bool bad = false;
-    bool loc[32] = {false};
-    for (size_t i = 0; i < n1[p] && !bad; ++i) {
-      const uint8_t c = sc->code[s1[p][i]];
-      if (c == 0xFF || c >= 32) bad = true; else loc[c] = true;
-    }
-    for (size_t j = 0; j < n2[p] && !bad; ++j) {
-      const uint8_t c = sc->code[s2[p][j]];
-      if (c == 0xFF || c >= 32) bad = true; else loc[c] = true;
-    }
-    if (bad) { h->prestatus[p] = BG_UNSCORABLE; continue; }
-    for (int c = 0; c < 32; ++c) present[c] |= loc[c];
   }
+  // the score closure's domain (score.rs:38-41 panics outside it): per pair, the set of codes its
+  // residues use, 0 bit 31 reserved for "a byte with no code" — one table lookup and OR per byte,
+  // pairs split over host threads by bytes
+  uint32_t bitOf[256];
+  for (int x = 0; x < 256; ++x) {
+    const uint8_t c = sc->code[x];
+    bitOf[x] = (c < 32) ? (1u << c) : 0x80000000u;
+  }
+  bool codeBad = false;                 // a byte coded 31 collides with the marker: scan exactly
+  for (int x = 0; x < 256; ++x) codeBad |= sc->code[x] == 31;
+  h->pmask.assign(npairs, 0);
+  par_ranges(npairs, [&](size_t p) -> uint64_t { return (uint64_t)n1[p] + n2[p]; },
+             [&](size_t lo, size_t hi) {
+    for (size_t p = lo; p < hi; ++p) {
+      if (h->prestatus[p] >= 0 || n1[p] == 0 || n2[p] == 0) continue;   // closure never called
+      uint32_t m = 0;
+      bool bad = false;
+      const uint8_t* x1 = s1[p];
+      const uint8_t* x2 = s2[p];
+      for (size_t i = 0; i < n1[p]; ++i) m |= bitOf[x1[i]];
+      for (size_t j = 0; j < n2[p]; ++j) m |= bitOf[x2[j]];
+      if (codeBad) {
+        for (size_t i = 0; i < n1[p] && !bad; ++i) bad = sc->code[x1[i]] >= 32;
+        for (size_t j = 0; j < n2[p] && !bad; ++j) bad = sc->code[x2[j]] >= 32;
+      } else {
+        bad = (m & 0x80000000u) != 0;
+      }
+      if (bad) h->prestatus[p] = BG_UNSCORABLE;
+      else h->pmask[p] = m;
+    }
+  });
+  for (size_t p = 0; p < npairs; ++p)
+    if (h->prestatus[p] < 0)
+      for (int c = 0; c < 32; ++c) present[c] |= ((h->pmask[p] >> c) & 1u) != 0;
 
   // ---- the reference's scratch history over the batch's calls (aligner.rs:92-94): the
   // argument errors return before the resize, everything else (the score panic included)
@@ -775,13 +855,13 @@ plan_again:
       return BG_E_NOMEM;
   }
 
-  // ---- uploads
-  std::vector<uint8_t> st1(o1 + 1), st2(o2 + 1);
-  for (size_t q = 0; q < order.size(); ++q) {
-    const size_t p = order[q];
-    if (n1[p]) std::memcpy(st1.data() + h->plan[q].off1, s1[p], n1[p]);
-    if (n2[p]) std::memcpy(st2.data() + h->plan[q].off2, s2[p], n2[p]);
-  }
+  // ---- uploads: raw residues and their codes staged in pinned host memory in plan order
+  // (pairs split over host threads by bytes), then one DMA each
+  if (!h->up.ensure(2 * (o1 + o2) + 64)) return BG_E_NOMEM;
+  uint8_t* st1 = h->up.as<uint8_t>();
+  uint8_t* st2 = st1 + o1 + 16;
+  uint8_t* cd1 = st2 + o2 + 16;
+  uint8_t* cd2 = cd1 + o1 + 16;
   uint8_t lut[256];
   for (int x = 0; x < 256; ++x) {
     const uint8_t c = sc->code[x];
@@ -829,13 +909,22 @@ plan_again:
       for (int c = 0; c < 32; ++c)
         if (dense[q] >= 0 && dense[c] >= 0) t16[dense[q] * 32 + dense[c]] = (int16_t)(sc->table[q * 32 + c] - a);
   }
-  std::vector<uint8_t> cd1(o1 + 1), cd2(o2 + 1);
-  for (uint64_t x = 0; x < o1; ++x) cd1[x] = lut[st1[x]];
-  for (uint64_t x = 0; x < o2; ++x) cd2[x] = lut[st2[x]];
-  BG_HIP(hipMemcpyAsync(h->seq1.p, st1.data(), o1 + 1, hipMemcpyHostToDevice, h->stream));
-  BG_HIP(hipMemcpyAsync(h->seq2.p, st2.data(), o2 + 1, hipMemcpyHostToDevice, h->stream));
-  BG_HIP(hipMemcpyAsync(h->codes1.p, cd1.data(), o1 + 1, hipMemcpyHostToDevice, h->stream));
-  BG_HIP(hipMemcpyAsync(h->codes2.p, cd2.data(), o2 + 1, hipMemcpyHostToDevice, h->stream));
+  par_ranges(order.size(), [&](size_t q) -> uint64_t { return (uint64_t)h->plan[q].n1 + h->plan[q].n2; },
+             [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q) {
+      const size_t p = order[q];
+      const BgPair& P = h->plan[q];
+      if (n1[p]) std::memcpy(st1 + P.off1, s1[p], n1[p]);
+      if (n2[p]) std::memcpy(st2 + P.off2, s2[p], n2[p]);
+      for (size_t x = 0; x < n1[p]; ++x) cd1[P.off1 + x] = lut[s1[p][x]];
+      for (size_t x = 0; x < n2[p]; ++x) cd2[P.off2 + x] = lut[s2[p][x]];
+    }
+  });
+  st1[o1] = st2[o2] = cd1[o1] = cd2[o2] = 0;
+  BG_HIP(hipMemcpyAsync(h->seq1.p, st1, o1 + 1, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->seq2.p, st2, o2 + 1, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->codes1.p, cd1, o1 + 1, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->codes2.p, cd2, o2 + 1, hipMemcpyHostToDevice, h->stream));
   BG_HIP(hipMemcpyAsync(h->lut.p, lut, 256, hipMemcpyHostToDevice, h->stream));
   BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), 2048, hipMemcpyHostToDevice, h->stream));
   if (!h->plan.empty())
@@ -1047,13 +1136,12 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   h->hres.resize(np);
   uint64_t ob = 0;
   for (const BgPair& P : h->plan) ob += (uint64_t)P.n1 + P.n2;
-  h->ho1.resize(ob + 1);
-  h->ho2.resize(ob + 1);
+  if (!h->ho1.ensure(ob + 1) || !h->ho2.ensure(ob + 1)) return BG_E_NOMEM;
   if (np) {
     const Slot& S = h->slot[h->lastSlot];
     BG_HIP(hipMemcpyAsync(h->hres.data(), S.results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, h->stream));
-    BG_HIP(hipMemcpyAsync(h->ho1.data(), S.out1.p, ob, hipMemcpyDeviceToHost, h->stream));
-    BG_HIP(hipMemcpyAsync(h->ho2.data(), S.out2.p, ob, hipMemcpyDeviceToHost, h->stream));
+    BG_HIP(hipMemcpyAsync(h->ho1.p, S.out1.p, ob, hipMemcpyDeviceToHost, h->stream));
+    BG_HIP(hipMemcpyAsync(h->ho2.p, S.out2.p, ob, hipMemcpyDeviceToHost, h->stream));
     BG_HIP(hipStreamSynchronize(h->stream));
   }
   for (size_t p = 0; p < h->npairs; ++p) {
@@ -1064,22 +1152,31 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   for (size_t q = 0; q < np; ++q) {
     const BgPair& P = h->plan[q];
     const BgResult& r = h->hres[q];
-    const size_t p = h->order_[q];
-    bg_pair_result& o = res[p];
-    o.status = r.status;
-    o.score = r.score;
-    o.len = r.out_len;
-    o.end_i = (uint32_t)r.end_i;
-    o.end_j = (uint32_t)r.end_j;
-    o.start1 = r.start1;
-    o.start2 = r.start2;
     if (r.out_len > (uint32_t)(P.n1 + P.n2) || r.out_start + r.out_len > (uint32_t)(P.n1 + P.n2)) return BG_E_HIP;
-    std::memcpy(out1 + h->outoff[p], h->ho1.data() + P.out_off + r.out_start, r.out_len);
-    std::memcpy(out2 + h->outoff[p], h->ho2.data() + P.out_off + r.out_start, r.out_len);
-    if (o.status == BG_OK && bg_ref_divergent(h->mode, (long)h->n1v[p], (long)h->n2v[p], r.score,
-                                              h->bufAt[p].first, h->bufAt[p].second))
-      o.status = BG_REF_DIVERGENT;
   }
+  const uint8_t* h1 = h->ho1.as<uint8_t>();
+  const uint8_t* h2 = h->ho2.as<uint8_t>();
+  par_ranges(np, [&](size_t q) -> uint64_t { return 2ull * h->hres[q].out_len + 64; },
+             [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q) {
+      const BgPair& P = h->plan[q];
+      const BgResult& r = h->hres[q];
+      const size_t p = h->order_[q];
+      bg_pair_result& o = res[p];
+      o.status = r.status;
+      o.score = r.score;
+      o.len = r.out_len;
+      o.end_i = (uint32_t)r.end_i;
+      o.end_j = (uint32_t)r.end_j;
+      o.start1 = r.start1;
+      o.start2 = r.start2;
+      std::memcpy(out1 + h->outoff[p], h1 + P.out_off + r.out_start, r.out_len);
+      std::memcpy(out2 + h->outoff[p], h2 + P.out_off + r.out_start, r.out_len);
+      if (o.status == BG_OK && bg_ref_divergent(h->mode, (long)h->n1v[p], (long)h->n2v[p], r.score,
+                                                h->bufAt[p].first, h->bufAt[p].second))
+        o.status = BG_REF_DIVERGENT;
+    }
+  });
   return BG_OK;
 }
 
