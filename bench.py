@@ -24,9 +24,10 @@ Fields beyond the driver's contract:
                   HBM peak 8 TB/s; `bound` names the roof that binds (VALU issue) and `valu`
                   its fraction: PMC-measured VALU instructions x 64 lanes / kernel time against
                   256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (MI355X_MICROARCH.md)
-  host_to_host    PCIe-inclusive rate: residues uploaded from host buffers, aligned strings
-                  downloaded to host buffers, two handles ping-ponged so one batch's upload and
-                  download overlap the other's kernels (never `value`)
+  host_to_host    PCIe-inclusive rate through the streaming API (biogarden_amd.stream): residues
+                  uploaded from host buffers, aligned strings downloaded to host buffers, four
+                  handles in rotation so batches' uploads and downloads overlap the kernels of
+                  the batches in flight (never `value`)
   cpu_baseline    the oracle (oracle/refcpu.c: the reference's six full matrices, its loop order,
                   one reused aligner per thread) on this host's cores, plus a 1-core rate and C1
 """
@@ -186,47 +187,32 @@ def timed(h, steps, warmup, barrier):
     return elapsed, dp_ms, fin_ms
 
 
-def host_to_host(native, pairs, sc, mode, a, b, device, rounds=6, pipeline=3):
-    """PCIe-inclusive throughput: per round one batch is prepared from host buffers (validation,
-    residue coding, H2D), executed, and fetched (D2H, aligned strings in host buffers).  Two
-    handles alternate so that batch k+1's upload runs while batch k is on the GPU and batch k's
-    download while k+1 is."""
-    hs = [native.Handle(device) for _ in range(2)]
-    for x in hs:
-        x.set_pipeline(pipeline)
-    try:
-        hs[0].prepare(mode, pairs, sc, a, b)          # warm the arenas of both handles
-        hs[0].execute()
-        hs[0].fetch()
-        hs[1].prepare(mode, pairs, sc, a, b)
-        hs[1].execute()
-        hs[1].fetch()
-        t_prep = t_fetch = 0.0
+def host_to_host(pairs, mode, a, b, device, rounds=8, pipeline=3, handles=4):
+    """PCIe-inclusive throughput through the product's streaming API (biogarden_amd.stream.
+    AlignStream): per batch the residues are staged from host buffers (validation, pinned
+    staging, H2D), the kernels run, and the aligned strings come back into host buffers; the
+    stream's handle rotation keeps `handles` batches in flight so uploads, downloads and the
+    host's byte passes overlap the kernels."""
+    from biogarden_amd.alignment import score
+    from biogarden_amd.stream import AlignStream
+    with AlignStream(mode, score.blosum62, a, b, device=device, handles=handles,
+                     pipeline=pipeline, raw=True) as st:
+        for _ in range(handles):                       # warm every handle's arenas
+            st.submit(pairs)
+        st.drain()
         t0 = time.perf_counter()
-        hs[0].prepare(mode, pairs, sc, a, b)
-        hs[0].execute()
-        for r in range(1, rounds + 1):
-            cur, prev = hs[r % 2], hs[(r - 1) % 2]
-            if r < rounds:
-                tp = time.perf_counter()
-                cur.prepare(mode, pairs, sc, a, b)
-                cur.execute()
-                t_prep += time.perf_counter() - tp
-            tf = time.perf_counter()
-            prev.fetch_raw()
-            t_fetch += time.perf_counter() - tf
+        done = 0
+        for r in range(rounds):
+            done += len(st.submit(pairs, tag=r))
+        done += len(st.drain())
         secs = time.perf_counter() - t0
-    finally:
-        for x in hs:
-            x.close()
+    assert done == rounds
     cells = workloads.cells(pairs)
-    return {"gcups": round(cells * rounds / secs / 1e9, 2), "rounds": rounds,
+    return {"gcups": round(cells * rounds / secs / 1e9, 2), "rounds": rounds, "handles": handles,
             "seconds_per_batch": round(secs / rounds, 5),
-            "host_prepare_s_per_batch": round(t_prep / max(rounds - 1, 1), 5),
-            "fetch_wait_s_per_batch": round(t_fetch / rounds, 5),
-            "covers": "bg_batch_prepare (validation, residue coding, H2D) + execute + "
-                      "bg_batch_fetch (D2H, aligned strings in caller buffers); two handles "
-                      "ping-ponged"}
+            "covers": "biogarden_amd.stream.AlignStream: bg_batch_prepare (validation, pinned "
+                      "staging, H2D) + execute + bg_batch_fetch (D2H, aligned strings in host "
+                      "buffers), %d handles in rotation" % handles}
 
 
 def cpu_section(pairs, gpu_scores, mode, a, b, info, pairs_multi, pairs_one):
@@ -287,6 +273,7 @@ def main():
     ap.add_argument("--no-affine", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host timing")
+    ap.add_argument("--h2h-handles", type=int, default=4)
     args = ap.parse_args()
 
     import torch
@@ -384,8 +371,8 @@ def main():
     # ---- host-to-host rate (not `value`): host buffers in, aligned strings back on the host
     h2h = None
     if not args.no_h2h:
-        h2h = host_to_host(_native, pairs, sc, args.mode, args.open, args.extend, local_rank,
-                           pipeline=args.pipeline)
+        h2h = host_to_host(pairs, args.mode, args.open, args.extend, local_rank,
+                           pipeline=args.pipeline, handles=args.h2h_handles)
 
     if rank != 0:
         h.close()

@@ -21,7 +21,8 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
            "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
            "bg_set_pipeline", "bg_set_kernel_options", "bg_edit_distance_batch",
-           "bg_lcs_batch", "bg_aligner_buffer_size"]
+           "bg_lcs_batch", "bg_aligner_buffer_size", "bg_aligner_set_buffer_size", "bg_fasta_open", "bg_fasta_next_batch",
+           "bg_fasta_close"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -52,6 +53,13 @@ class BgStats(ctypes.Structure):
                 ("checkpoint", ctypes.c_int32),
                 ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float),
                 ("fin_waves", ctypes.c_int32), ("fin_slots", ctypes.c_int32)]
+
+
+class BgFastaBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_size_t), ("seq", ctypes.c_void_p),
+                ("seq_off", ctypes.POINTER(ctypes.c_uint64)), ("text", ctypes.c_void_p),
+                ("id_off", ctypes.POINTER(ctypes.c_uint64)),
+                ("desc_off", ctypes.POINTER(ctypes.c_uint64))]
 
 
 _LIB = None
@@ -92,6 +100,7 @@ def lib():
     L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
     L.bg_aligner_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.c_size_t)]
+    L.bg_aligner_set_buffer_size.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t]
     L.bg_set_tuning.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     L.bg_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.bg_set_kernel_options.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -109,6 +118,13 @@ def lib():
     L.bg_edit_distance_batch.argtypes = pair_args + [ctypes.POINTER(ctypes.c_uint64)]
     L.bg_lcs_batch.argtypes = pair_args + [c_u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.POINTER(ctypes.c_uint64)]
+    L.bg_fasta_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
+    L.bg_fasta_open.restype = ctypes.c_void_p
+    L.bg_fasta_next_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                      ctypes.POINTER(BgFastaBatch)]
+    L.bg_fasta_next_batch.restype = ctypes.c_long
+    L.bg_fasta_close.argtypes = [ctypes.c_void_p]
+    L.bg_fasta_close.restype = None
     _LIB = L
     return L
 
@@ -168,6 +184,38 @@ class Handle:
         n1 = (ctypes.c_size_t * n)(*[len(x) for x in s1])
         n2 = (ctypes.c_size_t * n)(*[len(x) for x in s2])
         return a1, n1, a2, n2, sum(len(x) for x in s1) + sum(len(x) for x in s2)
+
+    @staticmethod
+    def _packed_arrays(buf1, off1, idx1, buf2, off2, idx2):
+        """Pointer + length arrays into two packed residue buffers (bytes objects, e.g. FASTA
+        batches): pair p is buf1[off1[idx1[p]]:off1[idx1[p]+1]] against the same in buf2.
+        No per-pair copy."""
+        import numpy as np
+        n = len(idx1)
+        b1 = ctypes.cast(ctypes.c_char_p(buf1), ctypes.c_void_p).value or 0
+        b2 = ctypes.cast(ctypes.c_char_p(buf2), ctypes.c_void_p).value or 0
+        o1, o2 = np.asarray(off1, dtype=np.uint64), np.asarray(off2, dtype=np.uint64)
+        i1, i2 = np.asarray(idx1, dtype=np.int64), np.asarray(idx2, dtype=np.int64)
+        p1 = (np.uint64(b1) + o1[i1]).astype(np.uint64)
+        p2 = (np.uint64(b2) + o2[i2]).astype(np.uint64)
+        l1 = (o1[i1 + 1] - o1[i1]).astype(np.uint64)
+        l2 = (o2[i2 + 1] - o2[i2]).astype(np.uint64)
+        a1 = (ctypes.c_uint64 * max(n, 1)).from_buffer_copy(p1.tobytes() or bytes(8))
+        a2 = (ctypes.c_uint64 * max(n, 1)).from_buffer_copy(p2.tobytes() or bytes(8))
+        n1 = (ctypes.c_size_t * max(n, 1)).from_buffer_copy(l1.tobytes() or bytes(8))
+        n2 = (ctypes.c_size_t * max(n, 1)).from_buffer_copy(l2.tobytes() or bytes(8))
+        return (ctypes.cast(a1, ctypes.POINTER(ctypes.c_char_p)), n1,
+                ctypes.cast(a2, ctypes.POINTER(ctypes.c_char_p)), n2,
+                int(l1.sum()) + int(l2.sum()), (buf1, buf2, a1, a2))
+
+    def prepare_packed(self, mode, buf1, off1, idx1, buf2, off2, idx2, scoring, a, b):
+        """prepare() for pairs given as indices into two packed residue buffers."""
+        a1, n1, a2, n2, total, keep = self._packed_arrays(buf1, off1, idx1, buf2, off2, idx2)
+        self._keep = (a1, n1, a2, n2, keep)
+        self._npairs = len(idx1)
+        self._total = total
+        check(lib().bg_batch_prepare(self._p, MODES.get(mode, mode), len(idx1), a1, n1, a2, n2,
+                                     ctypes.byref(scoring), a, b))
 
     def prepare(self, mode, pairs, scoring, a, b):
         a1, n1, a2, n2, total = self._arrays(pairs)
@@ -271,6 +319,9 @@ class Handle:
         check(lib().bg_aligner_buffer_size(self._p, ctypes.byref(r), ctypes.byref(c)))
         return r.value, c.value
 
+
+    def set_buffer_size(self, rows, cols):
+        check(lib().bg_aligner_set_buffer_size(self._p, rows, cols))
     def stats(self):
         st = BgStats()
         check(lib().bg_get_stats(self._p, ctypes.byref(st)))

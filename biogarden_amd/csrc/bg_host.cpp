@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -30,6 +31,7 @@ extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes(int win_bytes);
 extern "C" int bg_finish_window_bytes(int R, int affine, size_t npairs, int cus);
 extern "C" void* bg_export_kernel_ptr();
+extern "C" void* bg_code_kernel_ptr();
 extern "C" void* bg_global_score_kernel_ptr();
 extern "C" void* bg_dp_aff_kernel_ptr(int R, int local);
 extern "C" int bg_dp_aff_head_bytes(void);
@@ -89,13 +91,13 @@ struct PinBuf {
 inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
 // Host worker threads for the byte passes of prepare / fetch: at most 16 (a GPU's share of the
-// host's cores on the MI355X nodes), one per ~1 MiB of input, BG_HOST_THREADS overrides.
+// host's cores on the MI355X nodes), one per ~256 KiB of input, BG_HOST_THREADS overrides.
 int host_threads(uint64_t bytes) {
   int t = 16;
   if (const char* e = std::getenv("BG_HOST_THREADS")) t = std::max(1, std::atoi(e));
   const unsigned hw = std::thread::hardware_concurrency();
   if (hw) t = std::min<int>(t, (int)hw);
-  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)t, bytes / (1 << 20) + 1));
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)t, bytes / (256 << 10) + 1));
 }
 
 // Runs fn(lo, hi) over [0, n) split into contiguous ranges of about equal weight
@@ -119,6 +121,22 @@ void par_ranges(size_t n, Wt weight, F fn) {
   }
   for (auto& x : th) x.join();
 }
+
+// BG_PREPARE_TIMING: wall time of bg_batch_prepare's phases on stderr
+struct PhaseTimer {
+  bool on = std::getenv("BG_PREPARE_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  char buf[512];
+  int n = 0;
+  void mark(const char* what) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    n += std::snprintf(buf + n, sizeof(buf) - n > 0 ? sizeof(buf) - n : 0, " %s %.3f", what,
+                       std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+  ~PhaseTimer() { if (on) std::fprintf(stderr, "prepare ms:%s\n", buf); }
+};
 
 }  // namespace
 
@@ -187,6 +205,7 @@ struct bg_aligner {
   PinBuf ho1, ho2;                 // fetch: the slot's aligned strings, downloaded
   PinBuf up;                       // prepare: raw residues + codes of the batch, uploaded
   std::vector<uint32_t> pmask;     // prepare: per pair, the score codes its residues use
+  std::vector<uint64_t> coff1, coff2;   // prepare: caller-order offsets of the staged residues
 
   // The reference aligner's scratch dims (aligner.rs:30 buffer_size): 1024 x 1024 at
   // SequenceAligner::new (:44-55), reset to (len1+1, len2+1) by a call with len1 > rows ||
@@ -236,6 +255,8 @@ extern "C" const char* bg_status_string(int s) {
     case BG_E_HIP: return "HIP error";
     case BG_E_NOMEM: return "out of memory";
     case BG_E_SCORE_RANGE: return "score - open does not fit int16";
+    case BG_E_IO: return "cannot open file";
+    case BG_E_FORMAT: return "Expected > at record start.";
     case BG_E_NO_BATCH: return "no prepared batch";
     case BG_E_ALPHABET: return "more than 32 symbols";
     default: return "unknown";
@@ -585,9 +606,11 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   if (!h || !sc || mode < BG_GLOBAL || mode > BG_SEMIGLOBAL) return BG_E_ARG;
   if (npairs && (!s1 || !n1 || !s2 || !n2)) return BG_E_ARG;
   if (sc->alphabet_size < 0 || sc->alphabet_size > 32) return BG_E_ARG;
+  PhaseTimer tm;
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
+  tm.mark("sync");
   for (Slot& S : h->slot) S.inflight = false;
   h->execCount = 0;
   h->prepared = false;
@@ -627,14 +650,31 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   bool codeBad = false;                 // a byte coded 31 collides with the marker: scan exactly
   for (int x = 0; x < 256; ++x) codeBad |= sc->code[x] == 31;
   h->pmask.assign(npairs, 0);
+  // the raw residues go to pinned staging in caller order in the same pass (the plan's LPT
+  // order only permutes BgPair records, never the bytes): one read of the caller's buffers
+  h->coff1.resize(npairs + 1);
+  h->coff2.resize(npairs + 1);
+  h->coff1[0] = h->coff2[0] = 0;
+  for (size_t p = 0; p < npairs; ++p) {
+    const bool stage = h->prestatus[p] < 0;
+    h->coff1[p + 1] = h->coff1[p] + (stage ? n1[p] : 0);
+    h->coff2[p + 1] = h->coff2[p] + (stage ? n2[p] : 0);
+  }
+  const uint64_t o1 = h->coff1[npairs], o2 = h->coff2[npairs];
+  if (!h->up.ensure(o1 + o2 + 512)) return BG_E_NOMEM;
+  uint8_t* st1 = h->up.as<uint8_t>();
+  uint8_t* st2 = st1 + o1 + 16;
   par_ranges(npairs, [&](size_t p) -> uint64_t { return (uint64_t)n1[p] + n2[p]; },
              [&](size_t lo, size_t hi) {
     for (size_t p = lo; p < hi; ++p) {
-      if (h->prestatus[p] >= 0 || n1[p] == 0 || n2[p] == 0) continue;   // closure never called
+      if (h->prestatus[p] >= 0) continue;
+      if (n1[p]) std::memcpy(st1 + h->coff1[p], s1[p], n1[p]);
+      if (n2[p]) std::memcpy(st2 + h->coff2[p], s2[p], n2[p]);
+      if (n1[p] == 0 || n2[p] == 0) continue;   // the score closure is never called
       uint32_t m = 0;
       bool bad = false;
-      const uint8_t* x1 = s1[p];
-      const uint8_t* x2 = s2[p];
+      const uint8_t* x1 = st1 + h->coff1[p];
+      const uint8_t* x2 = st2 + h->coff2[p];
       for (size_t i = 0; i < n1[p]; ++i) m |= bitOf[x1[i]];
       for (size_t j = 0; j < n2[p]; ++j) m |= bitOf[x2[j]];
       if (codeBad) {
@@ -651,6 +691,7 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
     if (h->prestatus[p] < 0)
       for (int c = 0; c < 32; ++c) present[c] |= ((h->pmask[p] >> c) & 1u) != 0;
 
+  tm.mark("validate");
   // ---- the reference's scratch history over the batch's calls (aligner.rs:92-94): the
   // argument errors return before the resize, everything else (the score panic included)
   // resizes first.  Edit distance and LCS do not use a SequenceAligner.
@@ -733,6 +774,7 @@ plan_again:
     ckLimit = true;
     goto plan_again;
   }
+  tm.mark("plan");
   size_t lds = 0;
   if (h->tag) {
     // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
@@ -794,7 +836,7 @@ plan_again:
   h->plan.reserve(order.size());
   h->wgmap.clear();
   h->progWords = 0;
-  uint64_t o1 = 0, o2 = 0, tro = 0, bo = 0, ao = 0, oo = 0;
+  uint64_t tro = 0, bo = 0, ao = 0, oo = 0;
   h->cells = 0;
   for (size_t p : order) {
     BgPair P;
@@ -804,8 +846,8 @@ plan_again:
     P.index = (int32_t)h->plan.size();
     P.caller = (int32_t)p;
     P.caller_off = h->outoff[p];
-    P.off1 = o1; o1 += n1[p];
-    P.off2 = o2; o2 += n2[p];
+    P.off1 = h->coff1[p];
+    P.off2 = h->coff2[p];
     const bool dp = n1[p] > 0 && n2[p] > 0;
     P.nstrips = dp ? (int32_t)((n1[p] + 64 * R - 1) / (64 * R)) : 0;
     P.pad = P.nstrips * 64 * R - P.n1;
@@ -838,6 +880,7 @@ plan_again:
   h->bndBytes = bo * 4 * ((h->affine || h->ack) ? 2 : 1);
   h->resBytes = o1 + o2;
 
+  tm.mark("layout");
   // ---- device memory
   if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->codes1.ensure(o1 + 16) ||
       !h->codes2.ensure(o2 + 16) || !h->lut.ensure(256) ||
@@ -855,13 +898,9 @@ plan_again:
       return BG_E_NOMEM;
   }
 
-  // ---- uploads: raw residues and their codes staged in pinned host memory in plan order
-  // (pairs split over host threads by bytes), then one DMA each
-  if (!h->up.ensure(2 * (o1 + o2) + 64)) return BG_E_NOMEM;
-  uint8_t* st1 = h->up.as<uint8_t>();
-  uint8_t* st2 = st1 + o1 + 16;
-  uint8_t* cd1 = st2 + o2 + 16;
-  uint8_t* cd2 = cd1 + o1 + 16;
+  tm.mark("alloc");
+  // ---- uploads: the raw residues staged above (one DMA each), the tables; the codes are
+  // made on the device (bg_code_kernel)
   uint8_t lut[256];
   for (int x = 0; x < 256; ++x) {
     const uint8_t c = sc->code[x];
@@ -909,23 +948,23 @@ plan_again:
       for (int c = 0; c < 32; ++c)
         if (dense[q] >= 0 && dense[c] >= 0) t16[dense[q] * 32 + dense[c]] = (int16_t)(sc->table[q * 32 + c] - a);
   }
-  par_ranges(order.size(), [&](size_t q) -> uint64_t { return (uint64_t)h->plan[q].n1 + h->plan[q].n2; },
-             [&](size_t lo, size_t hi) {
-    for (size_t q = lo; q < hi; ++q) {
-      const size_t p = order[q];
-      const BgPair& P = h->plan[q];
-      if (n1[p]) std::memcpy(st1 + P.off1, s1[p], n1[p]);
-      if (n2[p]) std::memcpy(st2 + P.off2, s2[p], n2[p]);
-      for (size_t x = 0; x < n1[p]; ++x) cd1[P.off1 + x] = lut[s1[p][x]];
-      for (size_t x = 0; x < n2[p]; ++x) cd2[P.off2 + x] = lut[s2[p][x]];
-    }
-  });
-  st1[o1] = st2[o2] = cd1[o1] = cd2[o2] = 0;
+  st1[o1] = st2[o2] = 0;
+  std::memcpy(st2 + o2 + 16, lut, 256);
   BG_HIP(hipMemcpyAsync(h->seq1.p, st1, o1 + 1, hipMemcpyHostToDevice, h->stream));
   BG_HIP(hipMemcpyAsync(h->seq2.p, st2, o2 + 1, hipMemcpyHostToDevice, h->stream));
-  BG_HIP(hipMemcpyAsync(h->codes1.p, cd1, o1 + 1, hipMemcpyHostToDevice, h->stream));
-  BG_HIP(hipMemcpyAsync(h->codes2.p, cd2, o2 + 1, hipMemcpyHostToDevice, h->stream));
-  BG_HIP(hipMemcpyAsync(h->lut.p, lut, 256, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->lut.p, st2 + o2 + 16, 256, hipMemcpyHostToDevice, h->stream));
+  {
+    const uint8_t* r1 = h->seq1.as<uint8_t>();
+    uint8_t* c1 = h->codes1.as<uint8_t>();
+    size_t m1 = o1 + 1;
+    const uint8_t* r2 = h->seq2.as<uint8_t>();
+    uint8_t* c2 = h->codes2.as<uint8_t>();
+    size_t m2 = o2 + 1;
+    const uint8_t* lt = h->lut.as<uint8_t>();
+    void* args[] = {&r1, &c1, &m1, &r2, &c2, &m2, &lt};
+    const int blocks = (int)std::min<uint64_t>(4096, std::max<uint64_t>(1, (m1 + m2) / (16 * 256) + 2));
+    BG_HIP(hipLaunchKernel(bg_code_kernel_ptr(), dim3(blocks), dim3(256), args, 0, h->stream));
+  }
   BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), 2048, hipMemcpyHostToDevice, h->stream));
   if (!h->plan.empty())
     if (h->wide)
@@ -945,11 +984,14 @@ plan_again:
       BG_HIP(hipMemcpyAsync(h->recs.p, tmpl.data(), sizeof(BgPairResultDev) * npairs,
                             hipMemcpyHostToDevice, h->stream));
   }
+  tm.mark("queue");
   BG_HIP(hipStreamSynchronize(h->stream));
+  tm.mark("upload");
   h->order_ = order;
   h->bufRows = bufR;
   h->bufCols = bufC;
   fin_geom(h, h->plan.size(), &h->finWaves, &h->finSlots);
+  tm.mark("fin_geom");
   h->prepared = true;
   return BG_OK;
 }
@@ -1227,6 +1269,13 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->finish_ms = h->fin_ms;
   o->fin_waves = h->finWaves;
   o->fin_slots = h->finSlots;
+  return BG_OK;
+}
+
+extern "C" int bg_aligner_set_buffer_size(bg_aligner* h, size_t rows, size_t cols) {
+  if (!h || rows > 0x7FFFFFFF || cols > 0x7FFFFFFF) return BG_E_ARG;
+  h->bufRows = (long)rows;
+  h->bufCols = (long)cols;
   return BG_OK;
 }
 

@@ -417,6 +417,42 @@ __global__ __launch_bounds__(256) void bg_export_kernel(BgExportArgs E) {
 
 extern "C" void* bg_export_kernel_ptr() { return (void*)&bg_export_kernel; }
 
+// Residue coding on the device: codes[x] = lut[raw[x]] over both concatenated sequence sets
+// (the host uploads only the raw bytes, which the strings are built from anyway).  16 bytes per
+// lane, grid-stride; the 256-byte table is read through the scalar-free vector path from L1.
+__global__ __launch_bounds__(256) void bg_code_kernel(const uint8_t* __restrict__ raw1,
+                                                      uint8_t* __restrict__ cd1, size_t n1,
+                                                      const uint8_t* __restrict__ raw2,
+                                                      uint8_t* __restrict__ cd2, size_t n2,
+                                                      const uint8_t* __restrict__ lut) {
+  __shared__ uint8_t t[256];
+  t[threadIdx.x] = lut[threadIdx.x];
+  __syncthreads();
+  const size_t v1 = (n1 + 15) / 16, v2 = (n2 + 15) / 16;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t v = (size_t)blockIdx.x * blockDim.x + threadIdx.x; v < v1 + v2; v += stride) {
+    const bool first = v < v1;
+    const size_t base = (first ? v : v - v1) * 16;
+    const uint8_t* in = first ? raw1 : raw2;
+    uint8_t* out = first ? cd1 : cd2;
+    const size_t n = first ? n1 : n2;
+    if (base + 16 <= n) {
+      const uint4 w = *reinterpret_cast<const uint4*>(in + base);
+      const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+      uint32_t o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        o[k] = (uint32_t)t[ww[k] & 0xff] | ((uint32_t)t[(ww[k] >> 8) & 0xff] << 8) |
+               ((uint32_t)t[(ww[k] >> 16) & 0xff] << 16) | ((uint32_t)t[ww[k] >> 24] << 24);
+      *reinterpret_cast<uint4*>(out + base) = make_uint4(o[0], o[1], o[2], o[3]);
+    } else {
+      for (size_t x = base; x < n; ++x) out[x] = t[in[x]];
+    }
+  }
+}
+
+extern "C" void* bg_code_kernel_ptr() { return (void*)&bg_code_kernel; }
+
 // ------------------------------------------------------------------ instantiation table
 
 typedef void (*bg_dp_fn)(BgDpArgs);

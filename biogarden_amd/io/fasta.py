@@ -52,8 +52,15 @@ class Record:
         return ">%s\n%s\n" % (header, self._seq.decode())
 
 
+# char::is_whitespace (Unicode White_Space), which str::trim_end and the header's
+# splitn(2, char::is_whitespace) use (fasta.rs:110, :119); Python's str.isspace differs
+# (it also takes U+001C-001F)
+_WS = frozenset("\t\n\x0b\x0c\r \x85\xa0\u1680\u2000\u2001\u2002\u2003\u2004\u2005"
+                "\u2006\u2007\u2008\u2009\u200a\u2028\u2029\u202f\u205f\u3000")
+
+
 def _trim_end(s):
-    return s.rstrip()
+    return s.rstrip("".join(_WS))
 
 
 class Reader:
@@ -64,7 +71,7 @@ class Reader:
     @classmethod
     def from_file(cls, path):
         try:
-            return cls(open(path, "r", newline=""))
+            return cls(open(path, "r", newline="", encoding="utf-8"))
         except OSError as e:
             raise IOError("Failed to read fasta from %r" % (str(path),)) from e
 
@@ -78,7 +85,7 @@ class Reader:
             raise IOError("Expected > at record start.")
         head = _trim_end(self._line[1:])
         # splitn(2, char::is_whitespace): id is the text before the FIRST whitespace char
-        cut = next((i for i, ch in enumerate(head) if ch.isspace()), None)
+        cut = next((i for i, ch in enumerate(head) if ch in _WS), None)
         if cut is None:
             record._id, record._desc = head, None
         else:
@@ -133,6 +140,96 @@ class Writer:
 
     def close(self):
         self._w.close()
+
+
+class FastaBatch:
+    """One batch of records from BatchReader: residues back to back in `seq` (bytes), record r
+    at seq[offsets[r]:offsets[r+1]]; ids / descriptions as the reference's Record has them."""
+    __slots__ = ("seq", "offsets", "ids", "descs")
+
+    def __init__(self, seq, offsets, ids, descs):
+        self.seq = seq
+        self.offsets = offsets
+        self.ids = ids
+        self.descs = descs
+
+    def __len__(self):
+        return len(self.ids)
+
+    def sequence(self, r):
+        return self.seq[self.offsets[r]:self.offsets[r + 1]]
+
+    def records(self):
+        return [Record(self.ids[r], self.descs[r], self.sequence(r)) for r in range(len(self))]
+
+    def tile(self):
+        from ..ds.tile import Tile
+        t = Tile()
+        for r in range(len(self)):
+            t.push(Sequence(self.sequence(r), self.ids[r]))
+        return t
+
+
+class BatchReader:
+    """Streaming FASTA ingest for the batch aligner (native, libbiogarden_gpu.so bg_fasta_*):
+    the file is read in large blocks and returned as FastaBatch objects of at most
+    `max_records` records / about `max_residues` residues, with read_all's record rules
+    (fasta.rs:95-135).  Feed a batch to AlignStream / Handle.prepare_packed without per-record
+    copies."""
+
+    def __init__(self, path, max_records=65536, max_residues=64 << 20):
+        import ctypes
+        from .. import _native
+        self._n = _native
+        err = ctypes.c_int(0)
+        self._r = _native.lib().bg_fasta_open(str(path).encode(), ctypes.byref(err))
+        if not self._r:
+            raise IOError("Failed to read fasta from %r" % (str(path),))
+        self.max_records = max_records
+        self.max_residues = max_residues
+
+    def next_batch(self):
+        import ctypes
+        import numpy as np
+        b = self._n.BgFastaBatch()
+        rc = self._n.lib().bg_fasta_next_batch(self._r, self.max_records, self.max_residues,
+                                               ctypes.byref(b))
+        if rc < 0:
+            if rc == -8:
+                raise IOError("Expected > at record start.")
+            self._n.check(rc)
+        n = b.n
+        if n == 0:
+            return None
+        offs = np.ctypeslib.as_array(b.seq_off, shape=(n + 1,)).copy()
+        seq = ctypes.string_at(b.seq, int(offs[-1])) if offs[-1] else b""
+        ido = np.ctypeslib.as_array(b.id_off, shape=(n,))
+        dso = np.ctypeslib.as_array(b.desc_off, shape=(n,))
+        ids, descs = [], []
+        for r in range(n):
+            ids.append(ctypes.string_at(b.text + int(ido[r])).decode("utf-8", "surrogateescape"))
+            d = int(dso[r])
+            descs.append(None if d == 0xFFFFFFFFFFFFFFFF else
+                         ctypes.string_at(b.text + d).decode("utf-8", "surrogateescape"))
+        return FastaBatch(seq, offs, ids, descs)
+
+    def __iter__(self):
+        while True:
+            batch = self.next_batch()
+            if batch is None:
+                return
+            yield batch
+
+    def close(self):
+        if self._r:
+            self._n.lib().bg_fasta_close(self._r)
+            self._r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def read_tile(path):

@@ -1,0 +1,130 @@
+"""Streaming batch alignment on one GPU: FASTA -> packed residues -> HBM, overlapped with the
+kernels.
+
+`AlignStream` keeps a rotation of handles (`bg_aligner`, each with its own HIP streams and
+arenas).  Submitting batch k stages its residues in pinned memory and queues its upload and
+kernels on handle k mod H while batches k-1 .. k-H+1 are still on the GPU; the oldest batch is
+fetched (D2H of the aligned strings into host buffers) only when its handle comes round again.
+The host's byte passes, the PCIe copies and the kernels of different batches therefore overlap,
+and the GPU sees a steady queue of batches (bench.py's `host_to_host` leg measures it).
+
+    with AlignStream("semiglobal", score.blosum62, -1, -2) as st:
+        for reads in fasta.BatchReader("reads.fa", max_records=8192):
+            for tag, results in st.submit(pairs_for(reads), tag=...):
+                consume(tag, results)
+        for tag, results in st.drain():
+            consume(tag, results)
+
+Each result is the AlignmentResult of SequenceAligner.align_batch (score, aligned seq1,
+aligned seq2, .status, .end, .start).  Results come back in submission order.  The stream
+stands for ONE reference aligner: the scratch dims that decide the reference-divergence flag
+(status 4, aligner.rs:92-94) pass from handle to handle in submission order, so a stream
+flags exactly what one SequenceAligner fed the same batches flags.
+"""
+from collections import deque
+
+from . import _native
+from .alignment import score as _score
+from .alignment.aligner import AlignmentResult, _as_bytes
+from .ds.sequence import Sequence
+
+
+class AlignStream:
+    def __init__(self, mode, score, a, b, device=0, handles=4, pipeline=3, raw=False):
+        """raw=True: results are Handle.fetch_raw() records (status / score / offset / len
+        lists and the two string buffers, valid until the same handle is collected again)
+        instead of AlignmentResult objects — for throughput measurement (bench.py)."""
+        if handles < 1:
+            raise ValueError("handles must be >= 1")
+        self.raw = raw
+        self.mode, self.score, self.a, self.b = mode, score, int(a), int(b)
+        self._hs = [_native.Handle(device) for _ in range(handles)]
+        for h in self._hs:
+            h.set_pipeline(pipeline)
+        self._next = 0
+        self._inflight = deque()            # (handle index, tag, panics, pairs-or-None)
+        # the stream is ONE reference aligner: its scratch dims (aligner.rs:92-94, which decide
+        # the reference-divergence flag, status 4) pass from handle to handle in call order
+        self._buf = self._hs[0].buffer_size()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _collect(self):
+        hi, tag, panics, keys = self._inflight.popleft()
+        if self.raw:
+            return tag, self._hs[hi].fetch_raw()
+        out = self._hs[hi].fetch()
+        res = []
+        for p, r in enumerate(out):
+            if r["status"] == 0 and panics and keys is not None and \
+                    _score.pair_panics(panics, keys[p][0], keys[p][1]):
+                r = dict(r, status=_native.BG_UNSCORABLE)
+            res.append(AlignmentResult(r["score"], Sequence(r["aligned1"]), Sequence(r["aligned2"]),
+                                       r["status"], r["end"], r["start"]))
+        return tag, res
+
+    def _slot(self):
+        """The next handle of the rotation, after collecting the batch it still holds."""
+        ready = []
+        hi = self._next
+        if any(x[0] == hi for x in self._inflight):
+            while self._inflight and self._inflight[0][0] != hi:
+                ready.append(self._collect())
+            ready.append(self._collect())
+        self._next = (hi + 1) % len(self._hs)
+        return hi, ready
+
+    def submit(self, pairs, tag=None):
+        """Queues one batch of (seq1, seq2) pairs.  Returns the batches that had to be collected
+        to free a handle: a list of (tag, results), oldest first."""
+        pairs = [(_as_bytes(x), _as_bytes(y)) for x, y in pairs]
+        sc, panics = _score.tabulate(self.score, pairs)
+        hi, ready = self._slot()
+        h = self._hs[hi]
+        h.set_buffer_size(*self._buf)
+        h.prepare(self.mode, pairs, sc, self.a, self.b)
+        self._buf = h.buffer_size()
+        h.execute()
+        self._inflight.append((hi, tag, panics, pairs if panics else None))
+        return ready
+
+    def submit_packed(self, buf1, off1, idx1, buf2, off2, idx2, tag=None):
+        """Queues the pairs (buf1[off1[idx1[p]]:off1[idx1[p]+1]], the same in buf2) straight from
+        packed residue buffers — FastaBatch.seq / .offsets — with no per-pair copy."""
+        sc, panics = _score.tabulate(self.score, [(buf1, buf2)])
+        hi, ready = self._slot()
+        h = self._hs[hi]
+        h.set_buffer_size(*self._buf)
+        h.prepare_packed(self.mode, buf1, off1, idx1, buf2, off2, idx2, sc, self.a, self.b)
+        self._buf = h.buffer_size()
+        h.execute()
+        keys = None
+        if panics:
+            keys = [(buf1[off1[i]:off1[i + 1]], buf2[off2[j]:off2[j + 1]]) for i, j in zip(idx1, idx2)]
+        self._inflight.append((hi, tag, panics, keys))
+        return ready
+
+    def drain(self):
+        """Collects every batch still in flight: a list of (tag, results), oldest first."""
+        out = []
+        while self._inflight:
+            out.append(self._collect())
+        return out
+
+    def close(self):
+        for h in self._hs:
+            h.close()
+        self._hs = []
+        self._inflight.clear()
+
+
+def align_stream(mode, batches, score, a, b, **kw):
+    """Generator over (tag, results) for an iterable of (tag, pairs) batches, in order."""
+    with AlignStream(mode, score, a, b, **kw) as st:
+        for tag, pairs in batches:
+            yield from st.submit(pairs, tag=tag)
+        yield from st.drain()

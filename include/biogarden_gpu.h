@@ -60,7 +60,9 @@ enum {
   BG_E_NOMEM = -3,      /* device or host allocation failed */
   BG_E_SCORE_RANGE = -4,/* a substitution score minus the gap-open penalty does not fit int16 */
   BG_E_NO_BATCH = -5,   /* bg_batch_execute/fetch without a prepared batch */
-  BG_E_ALPHABET = -6    /* more than 32 distinct scorable symbols in one batch */
+  BG_E_ALPHABET = -6,   /* more than 32 distinct scorable symbols in one batch */
+  BG_E_IO = -7,         /* bg_fasta_open: the file cannot be opened */
+  BG_E_FORMAT = -8      /* bg_fasta_next_batch: "Expected > at record start." (fasta.rs:104-109) */
 };
 
 /* Scoring closure as data: code[byte] in [0, alphabet_size) or 0xFF when the closure would
@@ -153,6 +155,10 @@ int bg_get_stats(bg_aligner* h, bg_stats* out);
  * (:92-94, 594-602), as the reference's calls would.  Status BG_REF_DIVERGENT is judged against
  * the dims each call starts from. */
 int bg_aligner_buffer_size(bg_aligner* h, size_t* rows, size_t* cols);
+/* Sets those dims (takes effect at the next bg_batch_prepare): several handles that together
+ * stand for ONE reference aligner — the streaming rotation of biogarden_amd/stream.py — pass
+ * the state on in call order. */
+int bg_aligner_set_buffer_size(bg_aligner* h, size_t rows, size_t cols);
 
 /* Kernel timing over a region of executes (HIP events recorded on the handle's stream around
  * the DP and the finish kernel of every execute; up to 4096 executes per region).
@@ -197,6 +203,28 @@ int bg_edit_distance_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s
 int bg_lcs_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s1, const size_t* n1,
                  const uint8_t* const* s2, const size_t* n2, uint8_t* out, size_t out_cap,
                  uint64_t* offset, uint64_t* len);
+
+/* ---- Streaming FASTA ingest (io::fasta::Reader::read / read_all, src/io/fasta.rs:95-135).
+ * Records are returned in batches, residues back to back in one reader-owned buffer: record r
+ * is seq[seq_off[r] .. seq_off[r+1]), its id the NUL-terminated text + id_off[r], its
+ * description text + desc_off[r] or absent (desc_off[r] == UINT64_MAX).  The batch is valid
+ * until the next call.  A batch ends after max_records records or once max_residues residues
+ * are buffered; reading stops for good at EOF or at the first empty record (read_all's rule).
+ * The pointer + length arrays bg_batch_prepare takes are seq + seq_off[r], seq_off[r+1] -
+ * seq_off[r]: no per-record copy on the way to the GPU. */
+typedef struct bg_fasta bg_fasta;
+typedef struct bg_fasta_batch {
+  size_t n;                    /* records in this batch (0: the file is exhausted) */
+  const uint8_t* seq;
+  const uint64_t* seq_off;     /* n + 1 entries */
+  const char* text;
+  const uint64_t* id_off;      /* n entries */
+  const uint64_t* desc_off;    /* n entries, UINT64_MAX = no description */
+} bg_fasta_batch;
+bg_fasta* bg_fasta_open(const char* path, int* err);        /* err: 0, BG_E_ARG or BG_E_IO */
+long bg_fasta_next_batch(bg_fasta* r, size_t max_records, size_t max_residues,
+                         bg_fasta_batch* out);               /* records, or BG_E_* (< 0) */
+void bg_fasta_close(bg_fasta* r);
 
 const char* bg_status_string(int status);
 int bg_abi_version(void);
