@@ -21,7 +21,8 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
            "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
            "bg_set_pipeline", "bg_set_kernel_options", "bg_edit_distance_batch",
-           "bg_lcs_batch", "bg_aligner_buffer_size", "bg_aligner_set_buffer_size", "bg_fasta_open", "bg_fasta_next_batch",
+           "bg_lcs_batch", "bg_aligner_buffer_size", "bg_aligner_set_buffer_size", "bg_fasta_open",
+           "bg_batch_prepare_table", "bg_fasta_next_batch",
            "bg_fasta_close"]
 
 
@@ -32,6 +33,16 @@ class NativeUnavailable(RuntimeError):
 class BgScoring(ctypes.Structure):
     _fields_ = [("alphabet_size", ctypes.c_int32), ("code", ctypes.c_uint8 * 256),
                 ("table", ctypes.c_int32 * 1024)]
+
+
+class WideScoring:
+    """A score table over up to 256 codes (bg_batch_prepare_table): code[byte] (>= k: the
+    closure panics on that byte) and a k x k table, row = seq1 code."""
+
+    def __init__(self, code, k, table):
+        self.code = (ctypes.c_uint16 * 256)(*code)
+        self.k = k
+        self.table = (ctypes.c_int32 * (k * k))(*table)
 
 
 class BgPairResult(ctypes.Structure):
@@ -93,6 +104,9 @@ def lib():
     L.bg_align_batch.argtypes = batch_args + [ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
                                               ctypes.c_size_t]
     L.bg_batch_prepare.argtypes = batch_args
+    L.bg_batch_prepare_table.argtypes = batch_args[:7] + [
+        ctypes.POINTER(ctypes.c_uint16), ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+        ctypes.c_int32, ctypes.c_int32]
     L.bg_batch_execute.argtypes = [ctypes.c_void_p]
     L.bg_synchronize.argtypes = [ctypes.c_void_p]
     L.bg_batch_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
@@ -214,16 +228,21 @@ class Handle:
         self._keep = (a1, n1, a2, n2, keep)
         self._npairs = len(idx1)
         self._total = total
-        check(lib().bg_batch_prepare(self._p, MODES.get(mode, mode), len(idx1), a1, n1, a2, n2,
-                                     ctypes.byref(scoring), a, b))
+        check(self._prepare_call(mode, len(idx1), a1, n1, a2, n2, scoring, a, b))
+
+    def _prepare_call(self, mode, n, a1, n1, a2, n2, scoring, a, b):
+        if isinstance(scoring, WideScoring):
+            return lib().bg_batch_prepare_table(self._p, MODES.get(mode, mode), n, a1, n1, a2, n2,
+                                                scoring.code, scoring.k, scoring.table, a, b)
+        return lib().bg_batch_prepare(self._p, MODES.get(mode, mode), n, a1, n1, a2, n2,
+                                      ctypes.byref(scoring), a, b)
 
     def prepare(self, mode, pairs, scoring, a, b):
         a1, n1, a2, n2, total = self._arrays(pairs)
         self._keep = (a1, n1, a2, n2)
         self._npairs = len(pairs)
         self._total = total
-        check(lib().bg_batch_prepare(self._p, MODES.get(mode, mode), len(pairs), a1, n1, a2, n2,
-                                     ctypes.byref(scoring), a, b))
+        check(self._prepare_call(mode, len(pairs), a1, n1, a2, n2, scoring, a, b))
 
     def execute(self):
         check(lib().bg_batch_execute(self._p))

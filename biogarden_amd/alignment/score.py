@@ -57,7 +57,20 @@ def tabulate(score, pairs):
         ys.update(bytes(s2))
     syms = sorted(xs | ys)
     if len(syms) > 32:
-        raise ValueError("more than 32 distinct symbols")
+        # beyond the 32 x 32 bg_scoring: a k x k table over every byte the batch uses
+        k = len(syms)
+        code = [0xFFFF] * 256
+        for i, x in enumerate(syms):
+            code[x] = i
+        table = [0] * (k * k)
+        panics = set()
+        for x in sorted(xs):
+            for y in sorted(ys):
+                try:
+                    table[code[x] * k + code[y]] = int(score(x, y))
+                except Exception:
+                    panics.add((x, y))
+        return _native.WideScoring(code, k, table), panics
     sc = _native.BgScoring()
     sc.alphabet_size = len(syms)
     for x in range(256):

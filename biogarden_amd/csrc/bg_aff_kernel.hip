@@ -80,7 +80,7 @@ __global__ __launch_bounds__(1024) void bg_dp_aff_kernel(BgDpArgs A) {
 
   const uint8_t* c1 = A.codes1 + P.off1;
   const uint8_t* g2 = A.codes2 + P.off2;
-  const int16_t* tab = reinterpret_cast<const int16_t*>(A.profile);   // [q * 32 + cd]
+  const int16_t* tab = reinterpret_cast<const int16_t*>(A.profile);   // [q * pstride + cd]
   auto fetch_codes = [&](int c, int (&v)[3]) {
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(1024) void bg_dp_aff_kernel(BgDpArgs A) {
         unsigned v = 0;
 #pragma unroll
         for (int bb = 0; bb < 4; ++bb)
-          if (wd * 4 + bb < R) v |= ((unsigned)tab[qk[wd * 4 + bb] * 32 + cd] & 0xffu) << (8 * bb);
+          if (wd * 4 + bb < R) v |= ((unsigned)tab[qk[wd * 4 + bb] * A.pstride + cd] & 0xffu) << (8 * bb);
         profTab[(cd * 64 + lane) * RW + wd] = (int)v;
       }
     }

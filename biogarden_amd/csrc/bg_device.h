@@ -99,6 +99,7 @@ struct BgDpArgs {
   int32_t aux_lds_off;     // tagged kernel: per-wave area (boundary block, ring, profile, codes)
   const int2* wgmap;       // tagged kernel, WIDE mode: per workgroup (plan index, index in group)
   uint32_t* gprog;         // tagged kernel, WIDE mode: global per-wave progress counters
+  int32_t pstride;         // row stride of the int16 profile table (the batch's dense alphabet)
   unsigned long long* dbg; // optional per-wave timestamps of the first strip (env BG_DP_TIMING):
                            // [gw * 8 + k], k: 0 strip, 1 start, 2 chunk 0 done, 3 end, 4 waited
 };
@@ -133,6 +134,7 @@ struct BgFinishArgs {
   int32_t area_ints;
   int32_t flags;           // BG_FIN_* below
   int32_t nslots;          // checkpoint modes: recomputed-chunk slots in use (0: all)
+  int32_t pstride;         // row stride of the int16 profile table (affine checkpoint path)
 };
 
 // BgFinishArgs::flags

@@ -178,7 +178,7 @@ __device__ void build_prof_aff(const BgFinishArgs& F, const BgPair& P, int s, in
 #pragma unroll
       for (int bb = 0; bb < 4; ++bb) {
         const int k = wd * 4 + bb, i = rowbase + k + 1;
-        if (k < R) v |= ((unsigned)tab[(i <= n1 ? c1[i - 1] : 0) * 32 + cd] & 0xffu) << (8 * bb);
+        if (k < R) v |= ((unsigned)tab[(i <= n1 ? c1[i - 1] : 0) * F.pstride + cd] & 0xffu) << (8 * bb);
       }
       profTab[(cd * 64 + lane) * RW + wd] = (int)v;
     }

@@ -23,6 +23,7 @@
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
 extern "C" int bg_dp_has_R(int R, int affine, int local, int dna);
+extern "C" void* bg_dp_kernel_p32_ptr(int R, int affine, int local);
 extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt);
 extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode);
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
@@ -122,6 +123,17 @@ void par_ranges(size_t n, Wt weight, F fn) {
   for (auto& x : th) x.join();
 }
 
+// The score closure tabulated over the codes a batch may use: code[byte] (0xFFFF:
+// the closure panics on that byte, score.rs:40), tab[q * K + c].  The 32 x 32 bg_scoring and the
+// wide table of bg_batch_prepare_table (up to 256 codes: any byte alphabet, as the reference's
+// &dyn Fn(&u8, &u8) -> i32 and analysis::seq's raw-byte equality allow) both become this.
+struct HScore {
+  uint16_t code[256];
+  int K = 0;
+  std::vector<int32_t> tab;
+  int32_t at(int q, int c) const { return tab[(size_t)q * K + c]; }
+};
+
 // BG_PREPARE_TIMING: wall time of bg_batch_prepare's phases on stderr
 struct PhaseTimer {
   bool on = std::getenv("BG_PREPARE_TIMING") != nullptr;
@@ -181,6 +193,9 @@ struct bg_aligner {
   int allowCkpt = 1;
   int allowAck = 1;
   int ckpt = 0;                    // tagged path: score-only DP + checkpoint traceback
+  int p32 = 0;                     // mask kernel with int32 profile entries (S - a beyond int16)
+  int pstride = 32;                // int16 profile table row stride (the batch's dense alphabet, >= 32)
+  std::vector<uint64_t> pmaskW;    // prepare: 256-bit code sets per pair (alphabets beyond 32)
   int finFlags = 0;                // BG_FIN_* for the finish kernel (edit distance, LCS)
   int ack = 0;                     // affine / local path: score-only DP (bg_aff_kernel.hip) +
                                    // traceback over recomputed full-trace chunks
@@ -254,11 +269,11 @@ extern "C" const char* bg_status_string(int s) {
     case BG_E_ARG: return "bad argument";
     case BG_E_HIP: return "HIP error";
     case BG_E_NOMEM: return "out of memory";
-    case BG_E_SCORE_RANGE: return "score - open does not fit int16";
+    case BG_E_SCORE_RANGE: return "lengths beyond the LCS value frame";
     case BG_E_IO: return "cannot open file";
     case BG_E_FORMAT: return "Expected > at record start.";
     case BG_E_NO_BATCH: return "no prepared batch";
-    case BG_E_ALPHABET: return "more than 32 symbols";
+    case BG_E_ALPHABET: return "more than 32 symbols with scores beyond the 8-bit-code kernels";
     default: return "unknown";
   }
 }
@@ -423,6 +438,7 @@ static int vgprs_of(const void* fn) {
 static void* dp_fn(const bg_aligner* h, int R) {
   if (h->tag) return bg_dp_kernel_tag_ptr(R, 0, h->ckpt);
   if (h->ack) return bg_dp_aff_kernel_ptr(R, h->local);
+  if (h->p32) return bg_dp_kernel_p32_ptr(R, h->affine, h->local);
   return bg_dp_kernel_ptr(R, h->affine, h->local, h->dna);
 }
 static void* fin_fn(const bg_aligner* h, int R) {
@@ -475,19 +491,25 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   struct Cand { double T; int R, W, wps, row; };
   std::vector<Cand> cands;
   std::vector<int> start, end, diff;
+  // relax: no candidate leaves room for a finish workgroup beside the DP's (big alphabets: both
+  // hold a K x 64 profile table) — plan the DP alone; the finish then waits for LDS
+  for (int relax = 0; relax < 2 && cands.empty(); ++relax)
   for (int Rc : cand) {
     if (h->tuneR && Rc != h->tuneR) continue;
     const void* fn = dp_fn(h, Rc);
     if (!fn) continue;
+    // the affine-family kernels stage codes pre-scaled by 256 * RW bytes in u16: RW = 2 (R = 8)
+    // holds codes < 128 only
+    if (h->ack && h->kdim > 128 && Rc > 4) continue;
     const int vg = vgprs_of(fn);
-    const int fin = h->depth > 1 ? vgprs_of(fin_fn(h, Rc)) : 0;
+    const int fin = (h->depth > 1 && !relax) ? vgprs_of(fin_fn(h, Rc)) : 0;
     // LDS of one finish workgroup that must fit beside the DP's when pipelining
     size_t finLds = 0;
     if (h->depth > 1 || h->ack) {
       int win = 0, area = 0;
       finLds = fin_lds(h, Rc, np, &win, &area);
     }
-    const size_t finLdsRes = h->depth > 1 ? finLds : 0;   // must fit beside the DP's
+    const size_t finLdsRes = (h->depth > 1 && !relax) ? finLds : 0;   // must fit beside the DP's
     const int opsPerStep = h->ack ? (h->local ? 8 * Rc + 4 : 6 * Rc + 4)
                          : h->ckpt ? 2 * Rc + 2 : (h->tag ? 5 * Rc + 2 : (h->affine ? 18 * Rc + 16 : 8 * Rc + 12));
     const int S = maxn1 ? (int)((maxn1 + 64 * Rc - 1) / (64 * Rc)) : 1;
@@ -597,15 +619,17 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
     *Rout = pick->R;
     *Wout = pick->W;
     h->tagRow = pick->row;
+  } else if (h->ack && h->kdim > 128 && dp_fn(h, 4)) {
+    *Rout = 4;                           // one wave, the R the 8-bit codes allow
+    *Wout = 1;
   }
 }
 
-extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
-                                const size_t* n1, const uint8_t* const* s2, const size_t* n2,
-                                const bg_scoring* sc, int32_t a, int32_t b) {
-  if (!h || !sc || mode < BG_GLOBAL || mode > BG_SEMIGLOBAL) return BG_E_ARG;
+static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
+                        const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                        const HScore& S, int32_t a, int32_t b) {
+  if (!h || mode < BG_GLOBAL || mode > BG_SEMIGLOBAL || S.K < 1 || S.K > 256) return BG_E_ARG;
   if (npairs && (!s1 || !n1 || !s2 || !n2)) return BG_E_ARG;
-  if (sc->alphabet_size < 0 || sc->alphabet_size > 32) return BG_E_ARG;
   PhaseTimer tm;
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream));
@@ -632,7 +656,7 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
 
   // ---- per-pair validation, in the reference's order
   const bool needNonPos = mode == BG_GLOBAL || mode == BG_LOCAL || mode == BG_FITTING;
-  bool present[32] = {false};
+  std::vector<char> present(S.K, 0);
   for (size_t p = 0; p < npairs; ++p) {
     if ((n1[p] && !s1[p]) || (n2[p] && !s2[p])) return BG_E_ARG;
     if (n1[p] > 0x3FFFFFFF || n2[p] > 0x3FFFFFFF) return BG_E_ARG;
@@ -644,12 +668,14 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   // pairs split over host threads by bytes
   uint32_t bitOf[256];
   for (int x = 0; x < 256; ++x) {
-    const uint8_t c = sc->code[x];
-    bitOf[x] = (c < 32) ? (1u << c) : 0x80000000u;
+    const uint16_t c = S.code[x];
+    bitOf[x] = (c < 32 && c < S.K) ? (1u << c) : 0x80000000u;
   }
   bool codeBad = false;                 // a byte coded 31 collides with the marker: scan exactly
-  for (int x = 0; x < 256; ++x) codeBad |= sc->code[x] == 31;
+  for (int x = 0; x < 256; ++x) codeBad |= S.code[x] == 31;
+  const bool wideK = S.K > 32;          // codes beyond 31: 256-bit sets per pair
   h->pmask.assign(npairs, 0);
+  if (wideK) h->pmaskW.assign(npairs * 4, 0);
   // the raw residues go to pinned staging in caller order in the same pass (the plan's LPT
   // order only permutes BgPair records, never the bytes): one read of the caller's buffers
   h->coff1.resize(npairs + 1);
@@ -671,15 +697,30 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
       if (n1[p]) std::memcpy(st1 + h->coff1[p], s1[p], n1[p]);
       if (n2[p]) std::memcpy(st2 + h->coff2[p], s2[p], n2[p]);
       if (n1[p] == 0 || n2[p] == 0) continue;   // the score closure is never called
-      uint32_t m = 0;
-      bool bad = false;
       const uint8_t* x1 = st1 + h->coff1[p];
       const uint8_t* x2 = st2 + h->coff2[p];
+      bool bad = false;
+      if (wideK) {
+        uint64_t m4[4] = {0, 0, 0, 0};
+        for (int side = 0; side < 2 && !bad; ++side) {
+          const uint8_t* x = side ? x2 : x1;
+          const size_t n = side ? n2[p] : n1[p];
+          for (size_t i = 0; i < n; ++i) {
+            const uint16_t c = S.code[x[i]];
+            if (c >= S.K) { bad = true; break; }
+            m4[c >> 6] |= 1ull << (c & 63);
+          }
+        }
+        if (bad) h->prestatus[p] = BG_UNSCORABLE;
+        else for (int w = 0; w < 4; ++w) h->pmaskW[p * 4 + w] = m4[w];
+        continue;
+      }
+      uint32_t m = 0;
       for (size_t i = 0; i < n1[p]; ++i) m |= bitOf[x1[i]];
       for (size_t j = 0; j < n2[p]; ++j) m |= bitOf[x2[j]];
       if (codeBad) {
-        for (size_t i = 0; i < n1[p] && !bad; ++i) bad = sc->code[x1[i]] >= 32;
-        for (size_t j = 0; j < n2[p] && !bad; ++j) bad = sc->code[x2[j]] >= 32;
+        for (size_t i = 0; i < n1[p] && !bad; ++i) bad = S.code[x1[i]] >= 32 || S.code[x1[i]] >= S.K;
+        for (size_t j = 0; j < n2[p] && !bad; ++j) bad = S.code[x2[j]] >= 32 || S.code[x2[j]] >= S.K;
       } else {
         bad = (m & 0x80000000u) != 0;
       }
@@ -687,9 +728,14 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
       else h->pmask[p] = m;
     }
   });
-  for (size_t p = 0; p < npairs; ++p)
-    if (h->prestatus[p] < 0)
-      for (int c = 0; c < 32; ++c) present[c] |= ((h->pmask[p] >> c) & 1u) != 0;
+  for (size_t p = 0; p < npairs; ++p) {
+    if (h->prestatus[p] >= 0) continue;
+    if (wideK) {
+      for (int c = 0; c < S.K; ++c) present[c] |= ((h->pmaskW[p * 4 + (c >> 6)] >> (c & 63)) & 1u) != 0;
+    } else {
+      for (int c = 0; c < 32 && c < S.K; ++c) present[c] |= ((h->pmask[p] >> c) & 1u) != 0;
+    }
+  }
 
   tm.mark("validate");
   // ---- the reference's scratch history over the batch's calls (aligner.rs:92-94): the
@@ -706,25 +752,29 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   }
 
   // ---- dense alphabet, profile, kernel family
-  int dense[32];
+  const int KS = S.K;
+  std::vector<int> dense(KS);
   int K = 0;
-  for (int c = 0; c < 32; ++c) dense[c] = present[c] ? K++ : -1;
+  for (int c = 0; c < KS; ++c) dense[c] = present[c] ? K++ : -1;
   int32_t maxAbsS = 0;
-  for (int q = 0; q < 32; ++q)
-    for (int c = 0; c < 32; ++c)
-      if (present[q] && present[c]) maxAbsS = std::max<int32_t>(maxAbsS, std::abs(sc->table[q * 32 + c]));
+  for (int q = 0; q < KS; ++q)
+    for (int c = 0; c < KS; ++c)
+      if (present[q] && present[c]) maxAbsS = std::max<int32_t>(maxAbsS, std::abs(S.at(q, c)));
   bool dnaOK = K <= 4;
   bool i16OK = true;
-  for (int q = 0; q < 32; ++q)
-    for (int c = 0; c < 32; ++c) {
+  for (int q = 0; q < KS; ++q)
+    for (int c = 0; c < KS; ++c) {
       if (!present[q] || !present[c]) continue;
-      const int64_t v = (int64_t)sc->table[q * 32 + c] - (int64_t)a;
+      const int64_t v = (int64_t)S.at(q, c) - (int64_t)a;
       if (v < -128 || v > 127) dnaOK = false;
       if (v < -32768 || v > 32767) i16OK = false;
     }
-  if (!dnaOK && !i16OK) return BG_E_SCORE_RANGE;
+  // S - a beyond int16 (the reference's closure is any i32): the mask kernel with int32 profile
+  // entries (bg_dp_kernel<4, ..., P32>), which keeps the reference's wrapping i32 arithmetic
+  h->p32 = (!dnaOK && !i16OK) ? 1 : 0;
   h->dna = dnaOK ? 1 : 0;
   h->kdim = std::max(K, 1);
+  h->pstride = std::max(K, 32);         // row stride of the int16 profile table in HBM
   h->local = mode == BG_LOCAL;
 
   size_t maxn1 = 0, maxn2 = 0, ncomp = 0;
@@ -741,10 +791,10 @@ extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const ui
   // tagged linear kernel: values 4(M - a(i+j)) + tag must stay far from overflow and the
   // profile bytes 4(S-2a)-2 / -3 must fit int8
   bool tagOK = h->allowTag && !h->affine && mode != BG_LOCAL && dnaOK && bound < 134217728.0;
-  for (int q = 0; q < 32 && tagOK; ++q)
-    for (int c = 0; c < 32 && tagOK; ++c)
+  for (int q = 0; q < KS && tagOK; ++q)
+    for (int c = 0; c < KS && tagOK; ++c)
       if (present[q] && present[c]) {
-        const int64_t v = 4 * ((int64_t)sc->table[q * 32 + c] - 2 * (int64_t)a);
+        const int64_t v = 4 * ((int64_t)S.at(q, c) - 2 * (int64_t)a);
         if (v - 3 < -128 || v - 2 > 127) tagOK = false;
       }
   h->tag = tagOK ? 1 : 0;
@@ -755,13 +805,16 @@ plan_again:
   // S - a); values, and the finite -inf drifting by e = b - a per step, far from wrapping
   bool ackOK = !h->tag && h->allowAck && bound < 268435456.0 &&
                std::abs((double)b - (double)a) * ((double)maxn1 + (double)maxn2 + 2.0) < 268435456.0;
-  for (int q = 0; q < 32 && ackOK; ++q)
-    for (int c = 0; c < 32 && ackOK; ++c)
+  for (int q = 0; q < KS && ackOK; ++q)
+    for (int c = 0; c < KS && ackOK; ++c)
       if (present[q] && present[c]) {
-        const int64_t v = (int64_t)sc->table[q * 32 + c] - (mode == BG_LOCAL ? 1 : 2) * (int64_t)a;
+        const int64_t v = (int64_t)S.at(q, c) - (mode == BG_LOCAL ? 1 : 2) * (int64_t)a;
         if (v < -128 || v > 127) ackOK = false;
       }
   h->ack = (ackOK && !ckLimit) ? 1 : 0;
+  // more than 32 symbols in the batch: only the score-only affine-family kernels index their
+  // profile by a code of up to 8 bits (the mask-trace kernel's tables are 32 x 32)
+  if (K > 32 && !h->ack) return BG_E_ALPHABET;
 
   // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair, or a group
   // of workgroups per pair in the tagged kernel's WIDE mode)
@@ -802,11 +855,11 @@ plan_again:
       --W;
     }
   } else {
-    lds = 256;               // lut (+ int16 table and per-wave profiles on the LDS path)
+    lds = 256;               // lut (+ int16 / int32 table and per-wave profiles on the LDS path)
     if (!h->dna) {
-      const int WPE = (R + 1) / 2;
+      const int WPE = h->p32 ? R : (R + 1) / 2;
       for (;;) {
-        lds = 256 + 2048 + (size_t)W * h->kdim * 64 * WPE * 4;
+        lds = 256 + (h->p32 ? 4096 : 2048) + (size_t)W * h->kdim * 64 * WPE * 4;
         if (lds + 64 <= 160 * 1024 || W == 1) break;
         --W;
       }
@@ -884,7 +937,7 @@ plan_again:
   // ---- device memory
   if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->codes1.ensure(o1 + 16) ||
       !h->codes2.ensure(o2 + 16) || !h->lut.ensure(256) ||
-      !h->prof.ensure(2048) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
+      !h->prof.ensure(std::max<size_t>(4096, (size_t)h->pstride * h->pstride * 2 + 64)) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
       !h->wgmapBuf.ensure(sizeof(int2) * (h->wgmap.size() + 1)) ||
       !h->gprogBuf.ensure(4 * ((size_t)h->progWords + 1)))
     return BG_E_NOMEM;
@@ -903,50 +956,55 @@ plan_again:
   // made on the device (bg_code_kernel)
   uint8_t lut[256];
   for (int x = 0; x < 256; ++x) {
-    const uint8_t c = sc->code[x];
-    const int d = (c < 32 && dense[c] >= 0) ? dense[c] : 0;
+    const uint16_t c = S.code[x];
+    const int d = (c < KS && dense[c] >= 0) ? dense[c] : 0;
     lut[x] = (uint8_t)((h->dna && !h->ack) ? d * 8 : d);
   }
-  std::vector<int32_t> prof(512, 0);
+  std::vector<int32_t> prof(std::max<size_t>(1024, ((size_t)h->pstride * h->pstride + 1) / 2), 0);
   if (h->ack) {
     int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
     const int mult = mode == BG_LOCAL ? 1 : 2;
-    for (int q = 0; q < 32; ++q)
-      for (int c = 0; c < 32; ++c)
+    for (int q = 0; q < KS; ++q)
+      for (int c = 0; c < KS; ++c)
         if (dense[q] >= 0 && dense[c] >= 0)
-          t16[dense[q] * 32 + dense[c]] = (int16_t)(sc->table[q * 32 + c] - mult * a);
+          t16[dense[q] * h->pstride + dense[c]] = (int16_t)(S.at(q, c) - mult * a);
   } else if (h->dna) {
-    for (int q = 0; q < 32; ++q) {
+    for (int q = 0; q < KS; ++q) {
       if (dense[q] < 0) continue;
       uint32_t packed = 0;
-      for (int c = 0; c < 32; ++c) {
+      for (int c = 0; c < KS; ++c) {
         if (dense[c] < 0) continue;
-        const int v = sc->table[q * 32 + c] - a;
+        const int v = S.at(q, c) - a;
         packed |= (uint32_t)(uint8_t)(int8_t)v << (8 * dense[c]);
       }
       prof[dense[q]] = (int32_t)packed;
       if (h->tag) {
         uint32_t px = 0, py = 0;
-        for (int c = 0; c < 32; ++c) {
+        for (int c = 0; c < KS; ++c) {
           if (dense[c] < 0) continue;
-          const int v = 4 * (sc->table[q * 32 + c] - 2 * a);   // frame M - a*(i+j)
+          const int v = 4 * (S.at(q, c) - 2 * a);   // frame M - a*(i+j)
           px |= (uint32_t)(uint8_t)(int8_t)(v - 2) << (8 * dense[c]);
           py |= (uint32_t)(uint8_t)(int8_t)(v - 3) << (8 * dense[c]);
         }
         prof[64 + dense[q]] = (int32_t)px;
         prof[128 + dense[q]] = (int32_t)py;
         uint32_t pz = 0;                       // score-only pass: S - 2a, untagged
-        for (int c = 0; c < 32; ++c)
+        for (int c = 0; c < KS; ++c)
           if (dense[c] >= 0)
-            pz |= (uint32_t)(uint8_t)(int8_t)(sc->table[q * 32 + c] - 2 * a) << (8 * dense[c]);
+            pz |= (uint32_t)(uint8_t)(int8_t)(S.at(q, c) - 2 * a) << (8 * dense[c]);
         prof[192 + dense[q]] = (int32_t)pz;
       }
     }
+  } else if (h->p32) {
+    for (int q = 0; q < KS; ++q)
+      for (int c = 0; c < KS; ++c)
+        if (dense[q] >= 0 && dense[c] >= 0)
+          prof[dense[q] * 32 + dense[c]] = (int32_t)((uint32_t)S.at(q, c) - (uint32_t)a);
   } else {
     int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
-    for (int q = 0; q < 32; ++q)
-      for (int c = 0; c < 32; ++c)
-        if (dense[q] >= 0 && dense[c] >= 0) t16[dense[q] * 32 + dense[c]] = (int16_t)(sc->table[q * 32 + c] - a);
+    for (int q = 0; q < KS; ++q)
+      for (int c = 0; c < KS; ++c)
+        if (dense[q] >= 0 && dense[c] >= 0) t16[dense[q] * 32 + dense[c]] = (int16_t)(S.at(q, c) - a);
   }
   st1[o1] = st2[o2] = 0;
   std::memcpy(st2 + o2 + 16, lut, 256);
@@ -965,7 +1023,7 @@ plan_again:
     const int blocks = (int)std::min<uint64_t>(4096, std::max<uint64_t>(1, (m1 + m2) / (16 * 256) + 2));
     BG_HIP(hipLaunchKernel(bg_code_kernel_ptr(), dim3(blocks), dim3(256), args, 0, h->stream));
   }
-  BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), 2048, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), prof.size() * 4, hipMemcpyHostToDevice, h->stream));
   if (!h->plan.empty())
     if (h->wide)
     BG_HIP(hipMemcpyAsync(h->wgmapBuf.p, h->wgmap.data(), sizeof(int2) * h->wgmap.size(),
@@ -994,6 +1052,30 @@ plan_again:
   tm.mark("fin_geom");
   h->prepared = true;
   return BG_OK;
+}
+
+extern "C" int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
+                                const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                                const bg_scoring* sc, int32_t a, int32_t b) {
+  if (!h || !sc || sc->alphabet_size < 0 || sc->alphabet_size > 32) return BG_E_ARG;
+  HScore S;
+  S.K = 32;
+  for (int x = 0; x < 256; ++x) S.code[x] = sc->code[x] < 32 ? sc->code[x] : 0xFFFF;
+  S.tab.assign(sc->table, sc->table + 1024);
+  return prepare_impl(h, mode, npairs, s1, n1, s2, n2, S, a, b);
+}
+
+extern "C" int bg_batch_prepare_table(bg_aligner* h, int mode, size_t npairs,
+                                      const uint8_t* const* s1, const size_t* n1,
+                                      const uint8_t* const* s2, const size_t* n2,
+                                      const uint16_t* code, int32_t k, const int32_t* table,
+                                      int32_t a, int32_t b) {
+  if (!h || !code || !table || k < 1 || k > 256) return BG_E_ARG;
+  HScore S;
+  S.K = k;
+  for (int x = 0; x < 256; ++x) S.code[x] = code[x] < k ? code[x] : 0xFFFF;
+  S.tab.assign(table, table + (size_t)k * k);
+  return prepare_impl(h, mode, npairs, s1, n1, s2, n2, S, a, b);
 }
 
 extern "C" int bg_batch_execute(bg_aligner* h) {
@@ -1039,6 +1121,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.aux = S.aux.as<int32_t>();
     A.profile = h->prof.as<int32_t>();
     A.kdim = h->kdim;
+    A.pstride = h->pstride;
     A.open = h->a;
     A.ext = h->b;
     A.mode = h->mode;
@@ -1076,6 +1159,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.dbg = nullptr;
     F.bndX = S.bndX.as<int32_t>();
     F.kdim = h->kdim;
+    F.pstride = h->pstride;
     F.area_ints = 0;
     F.flags = h->finFlags;
     if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;
@@ -1363,24 +1447,18 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
 //     recomputes full-trace chunks.
 static int equality_scoring(size_t npairs, const uint8_t* const* s1, const size_t* n1,
                             const uint8_t* const* s2, const size_t* n2, int32_t match,
-                            int32_t mismatch, bg_scoring* sc) {
+                            int32_t mismatch, HScore* sc) {
   bool seen[256] = {false};
   for (size_t p = 0; p < npairs; ++p) {
     if ((n1[p] && !s1[p]) || (n2[p] && !s2[p])) return BG_E_ARG;
     for (size_t i = 0; i < n1[p]; ++i) seen[s1[p][i]] = true;
     for (size_t j = 0; j < n2[p]; ++j) seen[s2[p][j]] = true;
   }
-  std::memset(sc, 0, sizeof(*sc));
-  std::memset(sc->code, 0xFF, sizeof(sc->code));
   int k = 0;
-  for (int x = 0; x < 256; ++x)
-    if (seen[x]) {
-      if (k == 32) return BG_E_ALPHABET;
-      sc->code[x] = (uint8_t)k++;
-    }
-  sc->alphabet_size = std::max(k, 1);
-  for (int r = 0; r < 32; ++r)
-    for (int c = 0; c < 32; ++c) sc->table[r * 32 + c] = r == c ? match : mismatch;
+  for (int x = 0; x < 256; ++x) sc->code[x] = seen[x] ? (uint16_t)k++ : (uint16_t)0xFFFF;
+  sc->K = std::max(k, 1);
+  sc->tab.assign((size_t)sc->K * sc->K, mismatch);
+  for (int r = 0; r < sc->K; ++r) sc->tab[(size_t)r * sc->K + r] = match;
   return BG_OK;
 }
 
@@ -1402,11 +1480,11 @@ extern "C" int bg_edit_distance_batch(bg_aligner* h, size_t npairs, const uint8_
                                       const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                                       uint64_t* dist) {
   if (!h || (npairs && (!s1 || !n1 || !s2 || !n2 || !dist))) return BG_E_ARG;
-  bg_scoring sc;
+  HScore sc;
   int rc = equality_scoring(npairs, s1, n1, s2, n2, 0, -1, &sc);
   if (rc) return rc;
   h->finFlags = BG_FIN_SCORE_ONLY;
-  rc = bg_batch_prepare(h, BG_GLOBAL, npairs, s1, n1, s2, n2, &sc, -1, -1);
+  rc = prepare_impl(h, BG_GLOBAL, npairs, s1, n1, s2, n2, sc, -1, -1);
   if (!rc) rc = bg_batch_execute(h);
   std::vector<BgResult> res;
   if (!rc) rc = fetch_scores(h, res);
@@ -1427,14 +1505,14 @@ extern "C" int bg_lcs_batch(bg_aligner* h, size_t npairs, const uint8_t* const* 
   size_t need = 0;
   for (size_t p = 0; p < npairs; ++p) need += std::min(n1[p], n2[p]);
   if (need && (!out || out_cap < need)) return BG_E_ARG;
-  bg_scoring sc;
+  HScore sc;
   int rc = equality_scoring(npairs, s1, n1, s2, n2, 1, -1, &sc);
   if (rc) return rc;
   const int allowTag = h->allowTag, allowAck = h->allowAck;
   h->allowTag = 0;           // the LCS tie rule lives in the recomputing affine-family traceback
   h->allowAck = 1;
   h->finFlags = BG_FIN_LCS;
-  rc = bg_batch_prepare(h, BG_GLOBAL, npairs, s1, n1, s2, n2, &sc, 0, 0);
+  rc = prepare_impl(h, BG_GLOBAL, npairs, s1, n1, s2, n2, sc, 0, 0);
   if (!rc && !h->ack) rc = BG_E_SCORE_RANGE;          // sizes beyond the frame's range
   if (!rc) rc = bg_batch_execute(h);
   std::vector<bg_pair_result> res(npairs);

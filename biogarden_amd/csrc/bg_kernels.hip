@@ -67,7 +67,12 @@ struct Ctx {
 // last chunks: column n2 capture / validity; everything general).
 enum { VAR_FAST = 0, VAR_SEL = 1, VAR_EDGE = 2 };
 
-template <int R, bool AFFINE, bool LOCAL, bool DNA, int VAR>
+// per-lane LDS profile dwords per code: R int16 entries (two per dword), or R int32 entries
+// (P32: tables whose S - a leave the int16 range, which the reference's i32 closure allows)
+template <int R, bool P32>
+struct MaskWPE { static constexpr int v = P32 ? R : (R + 1) / 2; };
+
+template <int R, bool AFFINE, bool LOCAL, bool DNA, int VAR, bool P32 = false>
 __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx& C, int c, int bM,
                                           int bX, int cv) {
   const int a = C.a;
@@ -86,8 +91,12 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
     int topX = 0;
     if constexpr (AFFINE) topX = dpp_shr1(rdlane(bX, u), S.Xlast);
     S.code = dpp_shr1(rdlane(cv, u), S.code);
-    int lp[DNA ? 1 : (R + 1) / 2];
-    if constexpr (!DNA) {
+    int lp[DNA ? 1 : MaskWPE<R, P32>::v];
+    if constexpr (!DNA && P32) {
+      static_assert(R == 4, "the int32 profile is built for R = 4");
+      const int4 v = *reinterpret_cast<const int4*>(C.ldsProf + (S.code * BG_WAVE + lane) * 4);
+      lp[0] = v.x; lp[1] = v.y; lp[2] = v.z; lp[3] = v.w;
+    } else if constexpr (!DNA) {
       if constexpr (R == 8) {
         const int4 v = *reinterpret_cast<const int4*>(C.ldsProf + (S.code * BG_WAVE + lane) * 4);
         lp[0] = v.x; lp[1] = v.y; lp[2] = v.z; lp[3] = v.w;
@@ -108,6 +117,7 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
     for (int k = 0; k < R; ++k) {
       int sp;
       if constexpr (DNA) sp = sbfe(S.prof[k], S.code, 8);
+      else if constexpr (P32) sp = lp[k];
       else sp = sbfe(lp[k >> 1], (k & 1) * 16, 16);
       const int d = wadd(diag, sp);           // M(i-1,j-1) + S(seq1[i-1], seq2[j-1])
       const int yo = S.Ma[k];                 // M(i,j-1) + a
@@ -214,11 +224,13 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
 
 }  // namespace
 
-template <int R, bool AFFINE, bool LOCAL, bool DNA>
+template <int R, bool AFFINE, bool LOCAL, bool DNA, bool P32 = false>
 __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(BgDpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* sLut = smem;                                        // 256 B
   int16_t* sTab = reinterpret_cast<int16_t*>(smem + 256);      // 32x32 int16 (LDS path)
+  int32_t* sTab32 = reinterpret_cast<int32_t*>(smem + 256);    // 32x32 int32 (P32)
+  constexpr int TABB = P32 ? 4096 : 2048;
   const int lane = threadIdx.x & 63;
   const int W = blockDim.x >> 6;
   const int w = uni(threadIdx.x >> 6);
@@ -235,7 +247,9 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
     if (A.codes_in_lds)
       for (int x = threadIdx.x; x < Pp.n2; x += blockDim.x) sCodes[x] = g[x];
   }
-  if constexpr (!DNA) {
+  if constexpr (!DNA && P32) {
+    for (int x = threadIdx.x; x < 1024; x += blockDim.x) sTab32[x] = A.profile[x];
+  } else if constexpr (!DNA) {
     const int16_t* g = reinterpret_cast<const int16_t*>(A.profile);
     for (int x = threadIdx.x; x < 1024; x += blockDim.x) sTab[x] = g[x];
   }
@@ -250,7 +264,7 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
   const size_t stripDw = (size_t)NC * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE;
 
   int* ldsProf = nullptr;
-  if constexpr (!DNA) ldsProf = reinterpret_cast<int*>(smem + 256 + 2048) + (size_t)w * A.kdim * BG_WAVE * ((R + 1) / 2);
+  if constexpr (!DNA) ldsProf = reinterpret_cast<int*>(smem + 256 + TABB) + (size_t)w * A.kdim * BG_WAVE * MaskWPE<R, P32>::v;
 
   Ctx C;
   C.a = a; C.b = b; C.mode = mode;
@@ -295,7 +309,17 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
       S.tA[k] = 0; S.tB[k] = 0;
       if constexpr (LOCAL) { S.bestv[k] = (i <= n1) ? INT32_MIN : INT32_MAX; S.bpos[k] = 0; }
     }
-    if constexpr (!DNA) {
+    if constexpr (!DNA && P32) {
+      // per-lane table [code][lane] of R int32 S(q_k, code) - a
+      for (int cd = 0; cd < A.kdim; ++cd) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int i = C.rowbase + k + 1;
+          const int qq = (i <= n1) ? c1[i - 1] : 0;
+          ldsProf[(cd * BG_WAVE + lane) * R + k] = sTab32[qq * 32 + cd];
+        }
+      }
+    } else if constexpr (!DNA) {
       // per-lane table [code][lane] of R int16 S(q_k, code) - a, 2R bytes per entry
       constexpr int WPE = (R + 1) / 2;
       for (int cd = 0; cd < A.kdim; ++cd) {
@@ -341,9 +365,9 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
         if constexpr (AFFINE) bX = load_agent(A.bndX + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
       }
       const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
-      if (edge) run_chunk<R, AFFINE, LOCAL, DNA, VAR_EDGE>(S, C, c, bM, bX, cv);
-      else if (lastStrip && selRow) run_chunk<R, AFFINE, LOCAL, DNA, VAR_SEL>(S, C, c, bM, bX, cv);
-      else run_chunk<R, AFFINE, LOCAL, DNA, VAR_FAST>(S, C, c, bM, bX, cv);
+      if (edge) run_chunk<R, AFFINE, LOCAL, DNA, VAR_EDGE, P32>(S, C, c, bM, bX, cv);
+      else if (lastStrip && selRow) run_chunk<R, AFFINE, LOCAL, DNA, VAR_SEL, P32>(S, C, c, bM, bX, cv);
+      else run_chunk<R, AFFINE, LOCAL, DNA, VAR_FAST, P32>(S, C, c, bM, bX, cv);
       // publish: the chunk ends with the R trace stores of its second half; everything issued
       // before them (this chunk's boundary-row stores included) has reached L2 at vmcnt(R)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
@@ -472,6 +496,17 @@ typedef void (*bg_dp_fn)(BgDpArgs);
 
 BG_INST_R(4)
 BG_INST_R(8)
+// int32 profile entries (tables whose S - a leave int16): R = 4, every gap model and mode
+template __global__ void bg_dp_kernel<4, false, false, false, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<4, false, true, false, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<4, true, false, false, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<4, true, true, false, true>(BgDpArgs);
+
+extern "C" void* bg_dp_kernel_p32_ptr(int R, int affine, int local) {
+  if (R != 4) return nullptr;
+  if (affine) return local ? (void*)&bg_dp_kernel<4, true, true, false, true> : (void*)&bg_dp_kernel<4, true, false, false, true>;
+  return local ? (void*)&bg_dp_kernel<4, false, true, false, true> : (void*)&bg_dp_kernel<4, false, false, false, true>;
+}
 // metric-path (linear gaps, DNA register profile) kernels at extra strip heights: the planner
 // picks R so that a pair's strip count fills the workgroup's waves (DESIGN.md "Geometry")
 BG_INST(5, false, false, true)

@@ -58,9 +58,9 @@ enum {
   BG_E_ARG = -1,        /* bad argument (null pointer, capacity too small, unknown mode) */
   BG_E_HIP = -2,        /* HIP runtime failure */
   BG_E_NOMEM = -3,      /* device or host allocation failed */
-  BG_E_SCORE_RANGE = -4,/* a substitution score minus the gap-open penalty does not fit int16 */
+  BG_E_SCORE_RANGE = -4,/* LCS only: lengths beyond its value frame (scores beyond int16 run the int32-profile kernel) */
   BG_E_NO_BATCH = -5,   /* bg_batch_execute/fetch without a prepared batch */
-  BG_E_ALPHABET = -6,   /* more than 32 distinct scorable symbols in one batch */
+  BG_E_ALPHABET = -6,   /* more than 32 symbols in a batch whose scores the 8-bit-code kernels cannot take */
   BG_E_IO = -7,         /* bg_fasta_open: the file cannot be opened */
   BG_E_FORMAT = -8      /* bg_fasta_next_batch: "Expected > at record start." (fasta.rs:104-109) */
 };
@@ -119,6 +119,15 @@ int bg_align_batch(bg_aligner* h, int mode, size_t npairs, const uint8_t* const*
 int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
                      const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                      const bg_scoring* scoring, int32_t a, int32_t b);
+/* bg_batch_prepare with a score table of up to 256 codes (the reference's closure over any
+ * bytes, score.rs:38-41 / A.8): code[byte] < k selects row / column of table (k x k, row = seq1
+ * code), code[byte] >= k marks a byte the closure panics on (status BG_UNSCORABLE).  Batches
+ * using more than 32 codes run on the score-only affine-family kernels; BG_E_ALPHABET if their
+ * value range rules them out (scores minus twice the open penalty beyond int8). */
+int bg_batch_prepare_table(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
+                           const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                           const uint16_t* code, int32_t k, const int32_t* table, int32_t a,
+                           int32_t b);
 int bg_batch_execute(bg_aligner* h);
 int bg_batch_fetch(bg_aligner* h, bg_pair_result* results, uint8_t* out1, uint8_t* out2,
                    size_t out_cap);
@@ -189,8 +198,8 @@ int bg_set_kernel_options(bg_aligner* h, int allow_tagged);
 
 /* analysis::seq::edit_distance (src/analysis/seq.rs:105-130) for a batch of pairs: unit-cost
  * Levenshtein distance over raw bytes, dist[p] = the reference's Ok(usize).  Runs the global DP
- * (byte equality 0 / -1, open = extend = -1) score-only on the GPU.  BG_E_ALPHABET when the
- * batch holds more than 32 distinct byte values.  Replaces the prepared batch. */
+ * (byte equality 0 / -1, open = extend = -1) score-only on the GPU, any byte values (up to 256
+ * distinct per batch).  Replaces the prepared batch. */
 int bg_edit_distance_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s1,
                            const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                            uint64_t* dist);
@@ -198,8 +207,7 @@ int bg_edit_distance_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s
 /* processing::patterns::longest_common_subsequence (src/processing/patterns.rs:82-118) for a
  * batch: the reference's subsequence (its tie rules) of pair p is out[offset[p] .. +len[p]);
  * out_cap >= sum of min(n1, n2).  Global DP (byte equality +1 / -1, open = extend = 0) with the
- * LCS tie rule in the traceback.  BG_E_ALPHABET beyond 32 distinct bytes.  Replaces the
- * prepared batch.  shortest_common_supersequence (:198-235) is the host-side merge around it. */
+ * LCS tie rule in the traceback, any byte values.  Replaces the prepared batch.  shortest_common_supersequence (:198-235) is the host-side merge around it. */
 int bg_lcs_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s1, const size_t* n1,
                  const uint8_t* const* s2, const size_t* n2, uint8_t* out, size_t out_cap,
                  uint64_t* offset, uint64_t* len);

@@ -49,6 +49,11 @@ static inline uint8_t SQ(or_aligner* A, const uint8_t* s, size_t n, size_t idx_p
 }
 /* score closure, e.g. blosum62 (score.rs:38-41): table[(a-65),(b-65)], panics outside 'A'..'Z'. */
 static inline int32_t SC(or_aligner* A, const or_scoring* sc, uint8_t p, uint8_t q) {
+  if (sc->wide_k > 0) {
+    const int k = sc->wide_k, wp = sc->wide_code[p], wq = sc->wide_code[q];
+    if (wp >= k || wq >= k) or_panic(A, OR_PANIC_SCORE);
+    return sc->wide_table[(size_t)wp * k + wq];
+  }
   uint8_t cp = sc->code[p], cq = sc->code[q];
   if (cp == 0xFF || cq == 0xFF) or_panic(A, OR_PANIC_SCORE);
   return sc->table[cp * 32 + cq];
@@ -197,7 +202,7 @@ static void dp_fast(or_aligner* A, const uint8_t* s1, size_t n1, const uint8_t* 
 
 static void dp(or_aligner* A, const uint8_t* s1, size_t n1, const uint8_t* s2, size_t n2,
                const or_scoring* sc, int32_t a, int32_t b, int local) {
-  int fast = n1 < A->rows && n2 < A->cols;
+  int fast = n1 < A->rows && n2 < A->cols && sc->wide_k == 0;   /* wide tables: checked loop */
   if (fast && n1 > 0 && n2 > 0) {
     for (size_t i = 0; i < n1 && fast; ++i) fast = sc->code[s1[i]] != 0xFF;
     for (size_t j = 0; j < n2 && fast; ++j) fast = sc->code[s2[j]] != 0xFF;

@@ -42,11 +42,16 @@ enum {
 };
 
 /* Scoring closure as data: code[byte] = 0..k-1, or 0xFF when the closure panics on it;
- * table[c1*32 + c2] = S(byte1, byte2).  Same layout as bg_scoring in include/biogarden_gpu.h. */
+ * table[c1*32 + c2] = S(byte1, byte2).  Same layout as bg_scoring in include/biogarden_gpu.h.
+ * wide_k > 0 instead tabulates a closure over up to 256 codes (the form of
+ * bg_batch_prepare_table): wide_code[byte] (>= wide_k: panics), wide_table[c1*wide_k + c2]. */
 typedef struct or_scoring {
   int32_t alphabet_size;
   uint8_t code[256];
   int32_t table[32 * 32];
+  int32_t wide_k;
+  const uint16_t* wide_code;
+  const int32_t* wide_table;
 } or_scoring;
 
 typedef struct or_aligner or_aligner;

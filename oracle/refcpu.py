@@ -18,7 +18,29 @@ BUILTIN = {"blosum62": 0, "pam250": 1, "unit": 2}
 
 class OrScoring(ctypes.Structure):
     _fields_ = [("alphabet_size", ctypes.c_int32), ("code", ctypes.c_uint8 * 256),
-                ("table", ctypes.c_int32 * 1024)]
+                ("table", ctypes.c_int32 * 1024), ("wide_k", ctypes.c_int32),
+                ("wide_code", ctypes.POINTER(ctypes.c_uint16)),
+                ("wide_table", ctypes.POINTER(ctypes.c_int32))]
+
+
+def wide_scoring(fn, symbols):
+    """A closure S(byte1, byte2) tabulated over any byte set (up to 256 codes); bytes outside
+    `symbols` panic."""
+    syms = sorted(set(symbols))
+    k = len(syms)
+    code = (ctypes.c_uint16 * 256)(*([0xFFFF] * 256))
+    for i, x in enumerate(syms):
+        code[x] = i
+    table = (ctypes.c_int32 * (k * k))()
+    for i, x in enumerate(syms):
+        for j, y in enumerate(syms):
+            table[i * k + j] = int(fn(x, y))
+    sc = OrScoring()
+    sc.wide_k = k
+    sc.wide_code = code
+    sc.wide_table = table
+    sc._keep = (code, table)
+    return sc
 
 
 def build():

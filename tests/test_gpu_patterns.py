@@ -87,8 +87,24 @@ def test_long_pairs(oracle):
         [oracle.longest_common_subsequence(a, b) for a, b in pairs]
 
 
-def test_alphabet_limit():
-    from biogarden_amd import _native
-    from biogarden_amd.analysis.seq import edit_distance
-    with pytest.raises(RuntimeError, match="32"):
-        edit_distance(bytes(range(40)), bytes(range(40, 80)))
+@pytest.mark.parametrize("nsym", [33, 100, 256])
+def test_wide_byte_alphabets_vs_oracle(oracle, nsym):
+    """edit_distance / LCS / SCS over raw bytes (seq.rs:105-130, patterns.rs:82-118 compare bytes
+    for equality: any of the 256 values) with more than 32 distinct bytes in the batch: the
+    affine-family kernels with 8-bit codes (bg_batch_prepare_table's form)."""
+    from biogarden_amd.analysis.seq import edit_distance, edit_distance_batch
+    from biogarden_amd.processing.patterns import (longest_common_subsequence_batch,
+                                                   shortest_common_supersequence_batch)
+    rng = random.Random(nsym)
+    alpha = bytes(rng.sample(range(256), nsym))
+    pairs = []
+    for n1, n2 in ((0, 5), (1, 1), (40, 40), (300, 280), (1500, 900), (64, 65), (2100, 2300)):
+        s1 = rand_seq(rng, n1, alpha)
+        s2 = mutate(rng, s1, alpha, 0.3)[:n2] if rng.random() < 0.7 else rand_seq(rng, n2, alpha)
+        pairs.append((s1, s2))
+    assert edit_distance_batch(pairs) == [oracle.edit_distance(a, b) for a, b in pairs]
+    assert [bytes(x.chain) for x in longest_common_subsequence_batch(pairs)] == \
+        [oracle.longest_common_subsequence(a, b) for a, b in pairs]
+    assert [bytes(x.chain) for x in shortest_common_supersequence_batch(pairs)] == \
+        [oracle.shortest_common_supersequence(a, b) for a, b in pairs]
+    assert edit_distance(bytes(range(40)), bytes(range(40, 80))) == 40
