@@ -10,14 +10,19 @@
 // above), per-lane LDS profile entries selected by the column code, an all-lane LDS output ring.
 //
 // Values.
-//   global / fitting / overlap / semiglobal: the frame V' = V - a(i+j) for M, X and Y, in which
-//     X'(i,j) = max(M'(i-1,j), X'(i-1,j) + e)          e = b - a
-//     Y'(i,j) = max(M'(i,j-1), Y'(i,j-1) + e)
-//     M'(i,j) = max(M'(i-1,j-1) + S - 2a, X', Y')
-//   6 VALU ops per cell (v_add_u32_sdwa with the int8 profile byte, 2 x (v_add, v_max),
-//   v_max3).  -inf (X row 0, Y column 0, aligner.rs:49-50) is the finite kAffNeg: the host only
-//   takes this path when every value and kAffNeg + e * (n1 + n2) stay far from wrapping, so
-//   saturating_add (aligner.rs:443,447) never saturates and the frame is exact.
+//   global / fitting / overlap / semiglobal: the frame V~ = V - b(i+j) for M, X and Y, in which
+//   both extensions are free and the opening constant c = a - b lands once per cell, on M:
+//     O(i,j)  = M~(i,j) + c                               (the "opened" M, what is stored)
+//     X~(i,j) = max(O(i-1,j), X~(i-1,j))                  (M(i-1,j)+a vs X(i-1,j)+b, shifted)
+//     Y~(i,j) = max(O(i,j-1), Y~(i,j-1))
+//     M~(i,j) = max(O(i-1,j-1) + S - a - b, X~, Y~)
+//   5 VALU ops per cell (v_add_u32_sdwa with the int8 profile byte S - a - b, v_max, v_max,
+//   v_max3, v_add) against 6 in the frame V - a(i+j), where X and Y each paid an extension add.
+//   The trace bits compare the same pairs shifted by the same amount (x_trace 'I' iff
+//   O(i-1,j) < X~(i-1,j) iff M(i-1,j)+a < X(i-1,j)+b), so they are the reference's.  -inf
+//   (X row 0, Y column 0, aligner.rs:49-50) is the finite kAffNeg, which no longer drifts; the
+//   host only takes this path when every value stays far from wrapping, so saturating_add
+//   (aligner.rs:443,447) never saturates and the frame is exact.
 //   local: the frame cannot carry the clamp at 0, so values are kept as MA = M + a:
 //     X = max3(MA(i-1,j), X(i-1,j) + b, 0),  Y = max3(MA(i,j-1), Y(i,j-1) + b, 0)
 //     M = max3(MA(i-1,j-1) + S - a, X, Y),   best_k = max(best_k, M)
@@ -74,16 +79,17 @@ __device__ __forceinline__ int prof_word(const ProfV<RW>& P, int k) {
   return P.w[k >> 2];
 }
 
-// border M of column 0, row i, in the kernel's representation (aligner.rs:98-104, 163, 233-237)
+// border M of column 0, row i, in the kernel's representation (aligner.rs:98-104, 163, 233-237):
+// local M + a, otherwise O = M - b*i + (a - b)
 template <bool LOCAL>
 __device__ __forceinline__ int aff_col0(int mode, int i, int a, int b) {
   if constexpr (LOCAL) return a;
-  return wadd(col0_M(mode, i, a, b), -wmul(a, i));
+  return wadd(wadd(col0_M(mode, i, a, b), -wmul(b, i)), wadd(a, -b));
 }
 template <bool LOCAL>
 __device__ __forceinline__ int aff_row0(int mode, int j, int a, int b) {
   if constexpr (LOCAL) return a;
-  return wadd(row0_M(mode, j, a, b), -wmul(a, j));
+  return wadd(wadd(row0_M(mode, j, a, b), -wmul(b, j)), wadd(a, -b));
 }
 
 // One cell; returns M (local: M itself, S.M gets M + a).  x / y are X / Y of the cell.
@@ -106,7 +112,8 @@ __device__ __forceinline__ void aff_cell(int dIn, int pw, int sel, int mo, int x
 template <int R, bool LOCAL, int VAR>
 __device__ __forceinline__ void aff_chunk(AffStrip<R, LOCAL>& S, const AffCtx& C, int c) {
   const int a = C.a;
-  const int g = LOCAL ? C.b : C.e;          // extend increment in the kernel's representation
+  const int g = LOCAL ? C.b : 0;            // extend increment in the kernel's representation
+  const int oc = wadd(C.a, -C.b);           // non-local: the opening constant c = a - b
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
   constexpr int RW = AffW<R>::v;
@@ -143,6 +150,8 @@ __device__ __forceinline__ void aff_chunk(AffStrip<R, LOCAL>& S, const AffCtx& C
           // a tree that keeps every step's M live (spills)
           asm volatile("v_max_i32 %0, %0, %1" : "+v"(S.best[k]) : "v"(valid ? m : 0));
           m = m + a;
+        } else {
+          m = m + oc;                           // O(i,j)
         }
         S.M[k] = m;
         S.Y[k] = y;
@@ -170,7 +179,7 @@ __device__ __forceinline__ void aff_chunk(AffStrip<R, LOCAL>& S, const AffCtx& C
 #pragma unroll
               for (int k = 0; k < R; ++k) {
                 const int i = C.rowbase + k + 1;
-                if (i <= C.n1) C.lastcol[i] = wadd(S.M[k], wmul(a, i + C.n2));
+                if (i <= C.n1) C.lastcol[i] = wadd(wadd(S.M[k], -oc), wmul(C.b, i + C.n2));
               }
             }
           }
@@ -226,7 +235,8 @@ template <int R, bool LOCAL, bool FIRST, bool FIND, bool LCS = false>
 __device__ __forceinline__ void aff_recomp(AffStrip<R, LOCAL>& S, const AffCtx& C, int c,
                                            uint32_t* slot, int fq, int fl, int target, int& found) {
   const int a = C.a;
-  const int g = LOCAL ? C.b : C.e;
+  const int g = LOCAL ? C.b : 0;
+  const int oc = wadd(C.a, -C.b);
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
   constexpr int RW = AffW<R>::v;
@@ -278,7 +288,7 @@ __device__ __forceinline__ void aff_recomp(AffStrip<R, LOCAL>& S, const AffCtx& 
           if (k == fq && lane == fl && m == target && found < 0 && j >= 1 && j <= C.n2) found = j;
         }
         dIn = S.M[k];
-        const int mv = LOCAL ? m + a : m;
+        const int mv = LOCAL ? m + a : m + oc;
         S.M[k] = mv;
         S.Y[k] = y;
         mo = mv;

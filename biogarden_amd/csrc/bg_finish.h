@@ -35,6 +35,8 @@ __device__ __forceinline__ int lastrowM(const Fin& f, int j) {
   // the tagged kernel stores X forms 4*(M(n1,j) - a*(n1+j)) + 2
   // checkpoint mode (tag 2) stores M'(n1,j) = M(n1,j) - a*(n1+j) itself
   if (f.F->tag == 2) return wadd(v, wmul(f.a, f.n1 + j));
+  // affine checkpoint path, non-local: O(n1,j) = M(n1,j) - b(n1+j) + (a - b)
+  if (f.F->tag == 3) return wadd(wadd(v, -wadd(f.a, -f.b)), wmul(f.b, f.n1 + j));
   return f.F->tag ? wadd(v >> 2, wmul(f.a, f.n1 + j)) : wadd(v, -f.a);
 }
 __device__ __forceinline__ int lastcolM(const Fin& f, int i) {

@@ -808,7 +808,8 @@ plan_again:
   for (int q = 0; q < KS && ackOK; ++q)
     for (int c = 0; c < KS && ackOK; ++c)
       if (present[q] && present[c]) {
-        const int64_t v = (int64_t)S.at(q, c) - (mode == BG_LOCAL ? 1 : 2) * (int64_t)a;
+        // profile bytes: local S - a; otherwise S - a - b (the opened frame, bg_aff_common.h)
+        const int64_t v = (int64_t)S.at(q, c) - (int64_t)a - (mode == BG_LOCAL ? 0 : (int64_t)b);
         if (v < -128 || v > 127) ackOK = false;
       }
   h->ack = (ackOK && !ckLimit) ? 1 : 0;
@@ -963,11 +964,11 @@ plan_again:
   std::vector<int32_t> prof(std::max<size_t>(1024, ((size_t)h->pstride * h->pstride + 1) / 2), 0);
   if (h->ack) {
     int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
-    const int mult = mode == BG_LOCAL ? 1 : 2;
+    const int sub = mode == BG_LOCAL ? a : a + b;
     for (int q = 0; q < KS; ++q)
       for (int c = 0; c < KS; ++c)
         if (dense[q] >= 0 && dense[c] >= 0)
-          t16[dense[q] * h->pstride + dense[c]] = (int16_t)(S.at(q, c) - mult * a);
+          t16[dense[q] * h->pstride + dense[c]] = (int16_t)(S.at(q, c) - sub);
   } else if (h->dna) {
     for (int q = 0; q < KS; ++q) {
       if (dense[q] < 0) continue;
@@ -1180,7 +1181,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       const size_t lds = bg_finish_ack_lds_bytes(h->R, h->kdim, h->local, fns, fnw, &win, &area);
       F.win_bytes = win;
       F.area_ints = area;
-      F.tag = 2;
+      F.tag = h->local ? 2 : 3;          // 3: the opened frame's boundary rows (bg_aff_common.h)
       F.affine = 1;
       void* ffn = bg_finish_ack_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
