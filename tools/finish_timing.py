@@ -17,8 +17,10 @@ h.set_pipeline(1)
 h.set_kernel_options(True, bool(ck))
 if len(sys.argv) > 4:
     h.set_tuning(int(sys.argv[3]), int(sys.argv[4]))
-pairs = bench.make_pairs(npairs, 10000, 10000, bench.SEED)
-h.prepare("semiglobal", pairs, _native.builtin_scoring(_native.BG_BLOSUM62), -1, -2)
+L = int(os.environ.get("LEN", "10000"))
+pairs = bench.make_pairs(npairs, L, L, bench.SEED)
+ga, gb = (int(x) for x in os.environ.get("GAPS", "-1,-2").split(","))
+h.prepare("semiglobal", pairs, _native.builtin_scoring(_native.BG_BLOSUM62), ga, gb)
 h.execute()
 h.fetch()
 h.profile_begin()

@@ -2,6 +2,7 @@
 // per SIMD with 8 independent chains per wave and 4 waves per SIMD (16 waves per CU).
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 
 #define OPS(name, expr)                                                                      \
   __global__ void k_##name(int* out, int iters) {                                             \
@@ -77,6 +78,39 @@ OPS(mul_lo_u16, "v_mul_lo_u16 %0, %0, %1")
 OPS(max_f16, "v_max_f16 %0, %0, %1")
 OPS(add_f32, "v_add_f32 %0, %0, %1")
 
+
+// round 2: 16-bit forms and encodings for a half-width DP
+OPS(max3_i16, "v_max3_i16 %0, %0, %1, %2")
+OPS(add_u16_sdwa, "v_add_u16_sdwa %0, %0, sext(%1) dst_sel:WORD_0 dst_unused:UNUSED_PAD src0_sel:WORD_0 src1_sel:BYTE_1")
+OPS(max_i16_e64, "v_max_i16_e64 %0, %0, %1")
+OPS(max_i32_e64, "v_max_i32_e64 %0, %0, %1")
+OPS(add_u32_e64, "v_add_u32_e64 %0, %0, %1")
+OPS(max_i16_dpp, "v_max_i16_dpp %0, %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf")
+OPS(sub_u16, "v_sub_u16 %0, %0, %1")
+OPS(max_u16, "v_max_u16 %0, %0, %1")
+OPS(max_i32_sw, "v_max_i32 %0, %1, %0")
+OPS(pk_add_i16, "v_pk_add_i16 %0, %0, %1")
+OPS(max_i16_sdwa, "v_max_i16_sdwa %0, %0, %1 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1 src1_sel:WORD_1")
+OPS(add_u16_k, "v_add_u16 %0, 7, %0")
+OPS(min_i16, "v_min_i16 %0, %0, %1")
+OPS(med3_i16, "v_med3_i16 %0, %0, %1, %2")
+OPS(max3_u32, "v_max3_u32 %0, %0, %1, %2")
+OPS(subrev_u32, "v_subrev_u32 %0, %1, %0")
+OPS(mul_u32_u24, "v_mul_u32_u24 %0, %0, %1")
+OPS(max_f32_sw, "v_max_f32 %0, %1, %0")
+OPS(min_f32, "v_min_f32 %0, %0, %1")
+OPS(pk_max_f16, "v_pk_max_f16 %0, %0, %1")
+OPS(max_i16_mix, "v_max_i16 %0, %0, %1\n v_max_i32 %0, %0, %2")
+
+// op_sel (VOP3 16-bit half selects)
+OPS(add_u16_opsel, "v_add_i16 %0, %0, %1 op_sel:[0,1,0]")
+OPS(max_i16_opsel, "v_add_i16 %0, %0, %1")
+OPS(max_i16_opsel_d, "v_mad_u16 %0, %0, %1, %2 op_sel:[0,1,0,0]")
+OPS(add_u16_e64, "v_add_u16_e64 %0, %0, %1")
+OPS(add_i16_clamp, "v_add_i16 %0, %0, %1 clamp")
+OPS(sub_i16_clamp, "v_sub_i16 %0, %0, %1 clamp")
+OPS(max_i16_k, "v_max_i16 %0, -5, %0")
+
 typedef void (*kfn)(int*, int);
 static void run(const char* name, kfn f, int wavesPerCU) {
   int* d;
@@ -106,5 +140,10 @@ int main() {
   R(add_sdwa) R(add_sdwa_w) R(max_sdwa) R(mov_sdwa_pres) R(add3_u32) R(xor_b32) R(mov_b32) R(lshrrev)
   R(ashrrev) R(alignbit) R(or3_b32) R(and_or) R(cnd_e32) R(add_co) R(sub_co) R(max_i16) R(add_u16)
   R(min_i32) R(bfe_i32) R(add_k) R(and_k) R(max_k) R(sad_u8) R(pk_max_i16x) R(mul_lo_u16) R(max_f16) R(add_f32)
+  if (getenv("R2ONLY")) {}
+  R(max3_i16) R(add_u16_sdwa) R(max_i16_e64) R(max_i32_e64) R(add_u32_e64) R(max_i16_dpp) R(sub_u16)
+  R(max_u16) R(max_i32_sw) R(pk_add_i16) R(max_i16_sdwa) R(add_u16_k) R(min_i16) R(med3_i16)
+  R(max3_u32) R(subrev_u32) R(mul_u32_u24) R(max_f32_sw) R(min_f32) R(pk_max_f16) R(max_i16_mix)
+  R(add_u16_opsel) R(max_i16_opsel) R(max_i16_opsel_d) R(add_u16_e64) R(add_i16_clamp) R(sub_i16_clamp) R(max_i16_k)
   return 0;
 }
