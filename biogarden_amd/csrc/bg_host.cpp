@@ -362,11 +362,11 @@ extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
   } while (0)
 
 // Strip pipeline of one pair on `gw` waves: phases (64-step chunks) until its last strip ends.
-static int pipeline_phases(int S, int gw, int NC) {
+static int pipeline_phases(int S, int gw, int NC, int lag = 2) {
   std::vector<int> start(S), end(S);
   int P = 0;
   for (int s = 0; s < S; ++s) {
-    int st = s ? start[s - 1] + 2 : 0;
+    int st = s ? start[s - 1] + lag : 0;
     if (s >= gw) st = std::max(st, end[s - gw]);
     start[s] = st;
     end[s] = st + NC;
@@ -378,7 +378,10 @@ static int pipeline_phases(int S, int gw, int NC) {
 // WIDE planner (tagged kernel, few large pairs): each pair gets a group of workgroups of 4 waves
 // (one wave per SIMD, a lone wave issues fastest) in proportion to its cells, at most one wave
 // per strip and at most the CU count in all, so every group is resident at once.  R minimises
-// the slowest pair's pipeline: phases * 64 steps * (5R + 2) ops * ~4.5 cycles.
+// the slowest pair's pipeline: phases * 64 steps * the lone-wave step latency.  Measured on C3
+// (BG_DP_TIMING, conveyor step): ~48 + 10R cycles per step (the R-long v_max3 chain of a step
+// plus its DPP and two LDS reads) and a strip starting ~3 chunks after the one above (two for
+// the anti-diagonal skew and the block, one for the hand-off): R = 4-5 beats R = 2 and R = 8.
 static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t npairs, int* Rout,
                       int* Wout) {
   std::vector<size_t> comp;
@@ -407,7 +410,7 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
       int G = std::max(1, std::min((int)share, (S + W - 1) / W));
       groups[p] = G;
       const int NC = (int)(n2[p] / 64 + 2);
-      T = std::max(T, (double)pipeline_phases(S, G * W, NC) * 64.0 * (5 * Rc + 2) * 4.5);
+      T = std::max(T, (double)pipeline_phases(S, G * W, NC, 3) * 64.0 * (48.0 + 10.0 * Rc));
     }
     if (T < best) { best = T; bestR = Rc; bestGroups = groups; }
   }
@@ -1240,12 +1243,14 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
     std::vector<unsigned long long> d(8 * 4096);
     BG_HIP(hipMemcpy(d.data(), h->dpDbg.p, 64 * 4096, hipMemcpyDeviceToHost));
     unsigned long long t0 = ~0ull, tend = 0;
+    int nrec = 0;
     for (int g = 0; g < 4096; ++g)
-      if (d[8 * g + 1]) { t0 = std::min(t0, d[8 * g + 1]); tend = std::max(tend, d[8 * g + 3]); }
+      if (d[8 * g + 1]) { t0 = std::min(t0, d[8 * g + 1]); tend = std::max(tend, d[8 * g + 3]); ++nrec; }
     std::fprintf(stderr, "dp timing: span %.1f us\n", (tend - t0) * 0.01);
     for (int g = 0; g < 4096; ++g) {
       if (!d[8 * g + 1]) continue;
-      if (g % 16 && g + 1 < 4096 && d[8 * (g + 1) + 1]) continue;   // every 16th wave + the last
+      // every wave of a small group, else every 16th wave + the last
+      if (nrec > 64 && g % 16 && g + 1 < 4096 && d[8 * (g + 1) + 1]) continue;
       std::fprintf(stderr, "  wave %4d strip %4llu start %8.1f c0done %8.1f end %8.1f us  waited %10.0f of %10.0f cycles\n", g,
                    d[8 * g], (d[8 * g + 1] - t0) * 0.01, (d[8 * g + 2] - t0) * 0.01,
                    (d[8 * g + 3] - t0) * 0.01, (double)d[8 * g + 4], (double)d[8 * g + 5]);

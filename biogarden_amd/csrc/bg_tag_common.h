@@ -273,4 +273,85 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
   }
 }
 
+// v_mov_b32_dpp wave_shl:1 — lane r receives lane r+1; lane 63 keeps `old`.
+__device__ __forceinline__ int dpp_shl1(int old, int src) {
+  return __builtin_amdgcn_update_dpp(old, src, 0x130, 0xf, 0xf, false);
+}
+
+// Score-only step of a WIDE strip that hands its boundary row to another strip (C3: one wave per
+// SIMD, every step a dependent chain, so the LDS instructions per step are the step's latency,
+// tools/micro/lone_step.hip).  The row above and the row this strip hands down share ONE register
+// Q instead of a broadcast LDS read and a ring write per step:
+//   * at the chunk start Q[r] = the row above at column t0 + r (block c);
+//   * step u reads Q[0] (the DPP's old operand: lane 0's row above at column t0 + u), then shifts
+//     Q down one lane (wave_shl:1) and puts this wave's last-row value of the previous step
+//     (lane 63, column t0 + u - 64) into lane 63;
+//   * after 64 steps Q[r] = the last row at column t0 - 64 + r: block c - 1, final, ready to go to
+//     the consumer.  The caller stores it and loads the next incoming block.
+// Only the last strip, whose output row is row n1 (any lane), keeps the ring (score_chunk).
+template <int R, int VAR>
+__device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C, int c, int& Q) {
+  const int a = C.a;
+  const int t0 = c * BG_CHUNK;
+  const int lane = C.lane;
+  constexpr int RW = ProfW<R>::v;
+  constexpr int PF = 4;
+  int qCode[PF];
+  ProfV<RW> qP[PF];
+#pragma unroll
+  for (int d = 0; d < PF; ++d) {
+    qP[d] = load_prof<RW>(C.profLane + C.codeLane[d]);
+    qCode[d] = C.codeLane[PF + d];
+  }
+  const uint16_t* cl = C.codeLane + 2 * PF;
+#pragma unroll
+  for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h, cl += BG_TRACE_BLK) {
+#pragma unroll
+    for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
+      const int u = h * BG_TRACE_BLK + uu;
+      const int t = t0 + u;
+      const int slot = uu % PF;
+      const ProfV<RW> P = qP[slot];
+      qP[slot] = load_prof<RW>(C.profLane + qCode[slot]);
+      qCode[slot] = cl[uu];
+      const int topX = dpp_shr1(Q, S.Xlast);                  // M'(row above, j); lane 0: Q[0]
+      Q = dpp_shl1(S.Xlast, Q);                               // hand the last row down the conveyor
+      int dIn = S.topPrev;
+      int xo = topX;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int yo = S.Y[k];
+        const int d = add_sbyte(dIn, P.w[k >> 2], k & 3);
+        const int best = imax(imax(d, xo), yo);
+        dIn = yo;
+        xo = best;
+        S.Y[k] = best;
+      }
+      S.topPrev = topX;
+      S.Xlast = xo;
+      if constexpr (VAR == TV_EDGE) {
+        if (c == 0) {                                         // column 0 (aligner.rs:98-104)
+          const bool rst = (t == lane);
+#pragma unroll
+          for (int k = 0; k < R; ++k) {
+            const int i = C.rowbase + k + 1;
+            S.Y[k] = rst ? wadd(col0_M(C.mode, i, a, C.b), -wmul(a, i)) : S.Y[k];
+          }
+          S.Xlast = rst ? S.Y[R - 1] : S.Xlast;
+        }
+        if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {    // column n2: M(i, n2)
+          if (lane == t - C.n2) {
+#pragma unroll
+            for (int k = 0; k < R; ++k) {
+              const int i = C.rowbase + k + 1;
+              if (i <= C.n1) C.lastcol[i] = wadd(S.Y[k], wmul(a, i + C.n2));
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
 }  // namespace bgk

@@ -57,7 +57,26 @@ using namespace bgk;
 constexpr int kTagWaveInts = 64 + 128;   // boundary block + output ring (last-strip lanes below
                                          // row n1 write a workgroup-shared dummy ring)
 constexpr int kTagStageU16 = 192;
-constexpr int kMailSlots = 4;   // boundary blocks in flight between two waves of a workgroup
+#ifndef BG_MAIL_SLOTS
+#define BG_MAIL_SLOTS 4
+#endif
+constexpr int kMailSlots = BG_MAIL_SLOTS;   // boundary blocks in flight between two waves of a workgroup
+
+// Polling pauses.  WIDE runs one wave per SIMD: nothing else wants the issue slots, and every
+// poll's wake-up latency adds to the strip's pace whenever it has caught up with its producer
+// (the downstream strips of a chain of caught-up consumers slow down by that much per chunk), so
+// it spins; the many-wave path sleeps to leave the slots to the other waves.
+#ifndef BG_WIDE_SLEEP
+#define BG_WIDE_SLEEP 0
+#endif
+__device__ __forceinline__ void wide_poll_pause() {
+  if constexpr (BG_WIDE_SLEEP > 0) __builtin_amdgcn_s_sleep(BG_WIDE_SLEEP);
+}
+template <bool WIDE>
+__device__ __forceinline__ void poll_pause() {
+  if constexpr (WIDE) wide_poll_pause();
+  else __builtin_amdgcn_s_sleep(1);
+}
 
 template <int R>
 __host__ __device__ constexpr int tag_wave_ints() {
@@ -211,10 +230,14 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     if (hbmAhead) {
       if (0 < nblk)
         while ((int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < needBase + 1)
-          __builtin_amdgcn_s_sleep(2);
+          wide_poll_pause();
       nbV = load_agent(bndAbove);
       pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    // WIDE strips that hand their row down (every one but the last) run the one-register
+    // conveyor step (score_chunk_conv): no per-step LDS read of the row above, no ring write
+    const bool conv = WIDE && CKPT && !lastStrip;
+    int Q = 0;
     const bool dbgOn = A.dbg != nullptr && rho == 0 && pairIdx == 0 && gw < 4096;
     unsigned long long tWait = 0, tStart = dbgOn ? __builtin_amdgcn_s_memrealtime() : 0;
     const unsigned long long cStart = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
@@ -233,15 +256,21 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       const int jb = c * BG_CHUNK + lane;
       if (s == 0) {
         const int m0 = wadd(row0_M(mode, jb, a, b), -wmul(a, jb));          // M'(0, j)
-        waveLds[lane] = CKPT ? m0 : 4 * m0 + 2;                             // (X form)
-        C.bIn = waveLds;
+        if (conv) Q = m0;
+        else {
+          waveLds[lane] = CKPT ? m0 : 4 * m0 + 2;                           // (X form)
+          C.bIn = waveLds;
+        }
       } else if (hbmAhead) {
-        waveLds[lane] = nbV;                                                // block c
-        C.bIn = waveLds;
+        if (conv) Q = nbV;                                                  // block c
+        else {
+          waveLds[lane] = nbV;
+          C.bIn = waveLds;
+        }
         if (c + 1 < NC) {
           if (c + 1 < nblk) {
             while (pollV < needBase + c + 2) {
-              __builtin_amdgcn_s_sleep(2);
+              wide_poll_pause();
               pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           }
@@ -254,13 +283,17 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
           const int pw = mailIn ? prevW : (s - 1) % GW;
           if (WIDE && !mailIn) {
             while ((int)__hip_atomic_load(gProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
-              __builtin_amdgcn_s_sleep(2);
+              wide_poll_pause();
           } else {
             while (__hip_atomic_load(sProg + pw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-              __builtin_amdgcn_s_sleep(1);
+              poll_pause<WIDE>();
           }
         }
-        if (mailIn) {
+        if (mailIn && conv) {
+          // the block goes into the conveyor register now: the slot is free for the producer
+          Q = prevMail[(seq % kMailSlots) * 64 + lane];
+          if (lane == 0) __hip_atomic_store(sCons + w, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (mailIn) {
           C.bIn = prevMail + (seq % kMailSlots) * 64;
         } else {
           waveLds[lane] = load_agent(A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
@@ -273,7 +306,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       if (mailOut && c >= 1 && c - 1 < nblk) {
         const int needC = seq - kMailSlots;                      // consumer chunks finished
         while (__hip_atomic_load(sCons + w + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < needC)
-          __builtin_amdgcn_s_sleep(1);
+          poll_pause<WIDE>();
         C.mail = mailbox + ((seq - 1) % kMailSlots) * 64;
       }
       if (dbgOn) tWait += __builtin_amdgcn_s_memtime() - tw0;
@@ -283,7 +316,14 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
 #pragma unroll
         for (int k = 0; k < R; ++k) ck[k * BG_WAVE] = S.Y[k];
         ck[R * BG_WAVE] = S.topPrev;
-        if (edge) score_chunk<R, TV_EDGE, WIDE>(S, C, c);
+        if (conv) {
+          if (edge) score_chunk_conv<R, TV_EDGE>(S, C, c, Q);
+          else score_chunk_conv<R, TV_FAST>(S, C, c, Q);
+          if (c >= 1) {                                            // Q = block c - 1, final
+            if (C.mail) C.mail[lane] = Q;
+            __hip_atomic_store(C.bndOut + (c - 1) * BG_CHUNK + lane, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
+        } else if (edge) score_chunk<R, TV_EDGE, WIDE>(S, C, c);
         else if (lastStrip && selRow) score_chunk<R, TV_SEL, WIDE>(S, C, c);
         else if (R <= 4 && s == 0) {
           // row 0 above: M'(0, j) for j >= 1 is linear (semiglobal / local / overlap: M = 0;
@@ -326,7 +366,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
           if (lane == 0) __hip_atomic_store(sProg + w, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
-      if (mailIn && lane == 0)   // release: this chunk's reads of the slot are done
+      if (mailIn && !conv && lane == 0)   // release: this chunk's reads of the slot are done
         __hip_atomic_store(sCons + w, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (dbgOn && lane == 0) {
