@@ -250,8 +250,8 @@ def cpu_section(pairs, gpu_scores, mode, a, b, info, pairs_multi, pairs_one):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--pairs", type=int, default=256)
     ap.add_argument("--len1", type=int, default=10000)
     ap.add_argument("--len2", type=int, default=10000)
