@@ -165,6 +165,7 @@ struct bg_aligner {
   int cus = 256;
   hipStream_t stream = nullptr;    // uploads, DP kernels, downloads
   hipStream_t stream2 = nullptr;   // end cell + traceback kernels
+  hipStream_t stream3 = nullptr;   // WIDE batches: every other execute's traceback (see execute)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
   DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
   Slot slot[3];
@@ -290,7 +291,8 @@ extern "C" bg_aligner* bg_aligner_new(int device) {
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     h->cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess) {
     bg_aligner_free(h);
     return nullptr;
   }
@@ -310,6 +312,7 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+  if (h->stream3) (void)hipStreamSynchronize(h->stream3);
   for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs,
                     &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg}) d->release();
   for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
@@ -324,6 +327,7 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
     if (e) (void)hipEventDestroy(e);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
+  if (h->stream3) (void)hipStreamDestroy(h->stream3);
   delete h;
 }
 
@@ -348,7 +352,7 @@ extern "C" int bg_set_kernel_options(bg_aligner* h, int allow_tagged) {
 extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
   if (!h || depth < 1 || depth > 3) return BG_E_ARG;
   if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
-      hipStreamSynchronize(h->stream2) != hipSuccess)
+      hipStreamSynchronize(h->stream2) != hipSuccess || hipStreamSynchronize(h->stream3) != hipSuccess)
     return BG_E_HIP;
   h->depth = depth;
   h->prepared = false;   // arenas are sized at prepare time
@@ -637,6 +641,7 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
+  BG_HIP(hipStreamSynchronize(h->stream3));
   tm.mark("sync");
   for (Slot& S : h->slot) S.inflight = false;
   h->execCount = 0;
@@ -1137,8 +1142,16 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[1], h->stream));
   BG_HIP(hipEventRecord(S.dpDone, h->stream));
-  BG_HIP(hipStreamWaitEvent(h->stream2, S.dpDone, 0));
-  BG_HIP(hipEventRecord(e[2], h->stream2));
+  // The traceback stream.  A WIDE batch (a few long pairs: C3) is traceback-bound and its walks
+  // occupy a handful of CUs, so consecutive executes' tracebacks alternate between two streams
+  // and run side by side (each still waits for its own DP; the slot it reads is not reused before
+  // its finDone); the step then follows the DP.  Many-pair batches keep one stream: their finish
+  // workgroups fill the CUs beside the next DP as it is.
+  hipStream_t fs = h->stream2;
+  if (h->wide && (h->execCount & 1) && !std::getenv("BG_FINISH_TIMING") && !std::getenv("BG_ONE_FIN_STREAM"))
+    fs = h->stream3;
+  BG_HIP(hipStreamWaitEvent(fs, S.dpDone, 0));
+  BG_HIP(hipEventRecord(e[2], fs));
   if (np) {
     BgFinishArgs F;
     F.pairs = h->pairs.as<BgPair>();
@@ -1170,7 +1183,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     if (std::getenv("BG_FIN_SELFSERVE")) F.flags |= BG_FIN_SELFSERVE;
     if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(64 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
-      BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, h->stream2));
+      BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, fs));
     }
     void* args[] = {&F};
     int fnw = 4, fns = 0;
@@ -1178,7 +1191,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.nslots = fns;
     if (h->finFlags & BG_FIN_SCORE_ONLY) {
       BG_HIP(hipLaunchKernel(bg_global_score_kernel_ptr(), dim3((np + 255) / 256), dim3(256), args, 0,
-                             h->stream2));
+                             fs));
     } else if (h->ack) {
       int win = 0, area = 0;
       const size_t lds = bg_finish_ack_lds_bytes(h->R, h->kdim, h->local, fns, fnw, &win, &area);
@@ -1188,22 +1201,22 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       F.affine = 1;
       void* ffn = bg_finish_ack_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, h->stream2));
+      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
     } else if (h->ckpt) {
       int win = 0;
       const size_t lds = bg_finish_ck_lds_bytes(h->R, fns, fnw, &win);
       F.win_bytes = win;
       void* ffn = bg_finish_ck_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, h->stream2));
+      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
     } else {
       F.win_bytes = bg_finish_window_bytes(h->R, h->affine, np, h->cus);
       BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(h->R, h->affine, h->mode), dim3(np), dim3(256), args,
-                             bg_finish_lds_bytes(F.win_bytes), h->stream2));
+                             bg_finish_lds_bytes(F.win_bytes), fs));
     }
   }
-  BG_HIP(hipEventRecord(e[3], h->stream2));
-  BG_HIP(hipEventRecord(S.finDone, h->stream2));
+  BG_HIP(hipEventRecord(e[3], fs));
+  BG_HIP(hipEventRecord(S.finDone, fs));
   S.inflight = true;
   if (e[0] != h->ev[0]) {  // keep the last execute's events for bg_get_stats
     h->last[0] = e[0]; h->last[1] = e[1]; h->last[2] = e[2]; h->last[3] = e[3];
@@ -1221,6 +1234,7 @@ extern "C" int bg_synchronize(bg_aligner* h) {
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
+  BG_HIP(hipStreamSynchronize(h->stream3));
   if (h->executed) {
     (void)hipEventElapsedTime(&h->dp_ms, h->last[0], h->last[1]);
     (void)hipEventElapsedTime(&h->fin_ms, h->last[2], h->last[3]);
@@ -1393,6 +1407,7 @@ extern "C" int bg_profile_end(bg_aligner* h, float* avg_dp, float* avg_fin, int*
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
+  BG_HIP(hipStreamSynchronize(h->stream3));
   double dp = 0, fin = 0;
   const int cnt = h->ringUsed / 4;
   for (int i = 0; i < cnt; ++i) {
@@ -1418,6 +1433,7 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   if (!h->executed) return BG_E_NO_BATCH;
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream2));
+  BG_HIP(hipStreamSynchronize(h->stream3));
   const Slot& S = h->slot[h->lastSlot];
   const uint64_t n = h->npairs;
   BG_HIP(hipMemcpyAsync(dst, &n, 8, hipMemcpyHostToDevice, h->stream));
