@@ -169,7 +169,8 @@ struct bg_aligner {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
   DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
   Slot slot[3];
-  int depth = 2;                   // pipeline depth (1 or 2 slots)
+  int depth = 3;                   // pipeline depth: arena slots in flight (1..3; 3 lets the
+                                   // traceback of step k overlap the DPs of k+1 and k+2)
   int execCount = 0;
   int lastSlot = 0;
 

@@ -54,9 +54,9 @@ def config(name, rng):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("configs", nargs="*", default=["C2", "C4", "C5", "C3"])
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--check", type=int, default=0)
-    ap.add_argument("--pipeline", type=int, default=2)
+    ap.add_argument("--pipeline", type=int, default=3)
     ap.add_argument("--R", type=int, default=0)
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--kernel-options", type=int, default=7)
