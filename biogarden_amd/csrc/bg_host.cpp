@@ -933,7 +933,20 @@ plan_again:
     P.buf_rows = (int32_t)std::min<long>(h->bufAt[p].first, 0x7FFFFFFF);
     P.buf_cols = (int32_t)std::min<long>(h->bufAt[p].second, 0x7FFFFFFF);
     if (h->wide) {
-      for (int g = 0; g < P.wg_count; ++g) h->wgmap.push_back(make_int2((int)h->plan.size(), g));
+      // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8
+      // share one, MI355X_MICROARCH.md), so consecutive indices in the group (consecutive strips:
+      // a boundary row handed through HBM) go to blocks of one XCD class, and the hand-offs stay
+      // inside one XCD's L2 except at the seven class boundaries.  BG_WIDE_LINEAR: plain order.
+      const int b0 = (int)h->wgmap.size(), G = P.wg_count;
+      const bool linear = std::getenv("BG_WIDE_LINEAR") != nullptr;
+      int cls[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int g = 0; g < G; ++g) ++cls[(b0 + g) & 7];
+      int first[8], seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int x = 0, acc = 0; x < 8; ++x) { first[(b0 + x) & 7] = acc; acc += cls[(b0 + x) & 7]; }
+      for (int g = 0; g < G; ++g) {
+        const int x = (b0 + g) & 7;
+        h->wgmap.push_back(make_int2((int)h->plan.size(), linear ? g : first[x] + seen[x]++));
+      }
       h->progWords += (uint32_t)(P.wg_count * W);
     }
     h->cells += (uint64_t)n1[p] * n2[p];
@@ -1149,7 +1162,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   // its finDone); the step then follows the DP.  Many-pair batches keep one stream: their finish
   // workgroups fill the CUs beside the next DP as it is.
   hipStream_t fs = h->stream2;
-  if (h->wide && (h->execCount & 1) && !std::getenv("BG_FINISH_TIMING") && !std::getenv("BG_ONE_FIN_STREAM"))
+  if ((h->wide || std::getenv("BG_TWO_FIN_STREAMS")) && (h->execCount & 1) && !std::getenv("BG_FINISH_TIMING") &&
+      !std::getenv("BG_ONE_FIN_STREAM"))
     fs = h->stream3;
   BG_HIP(hipStreamWaitEvent(fs, S.dpDone, 0));
   BG_HIP(hipEventRecord(e[2], fs));
