@@ -465,6 +465,11 @@ static void fin_geom(const bg_aligner* h, size_t np, int* nw, int* nslots) {
   // (tools/fin_geom_sweep.sh: one wave / two slots C2 1 266, C4 5 630, C5 2 274 GCUPS; two waves /
   // three slots 1 269, 6 017, 2 396; four waves 1 298, 6 039, 2 123)
   if ((h->ack || h->ckpt) && np > (size_t)h->cus * 2) { *nw = 2; *nslots = 3; }
+  // local (affine checkpoint) batches: one wave and two slots, the walker recomputing its own
+  // misses — more walks per CU beside the DP (tools/fin_geom_np.py at three pipeline slots: C2
+  // shape 1 548 -> 1 656 / 1 767 -> 1 854 GCUPS at 1 024 / 4 096 pairs; the C5 shape, global
+  // protein, loses with it: 2 576 -> 2 490)
+  if (h->ack && h->local && np > (size_t)h->cus * 2) { *nw = 1; *nslots = 2; }
   if (const char* e = std::getenv("BG_FIN_WAVES")) *nw = std::min(4, std::max(1, std::atoi(e)));
   if (const char* e = std::getenv("BG_FIN_SLOTS")) *nslots = std::max(0, std::atoi(e));
   if (*nslots && *nslots < *nw + 1) *nslots = *nw + 1;

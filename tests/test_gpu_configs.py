@@ -68,9 +68,9 @@ def test_C2_1024_local_dna_full_batch(aligner, oracle):
     res = check_batch(aligner, oracle, "local", pairs, "blosum62", -11, -1,
                       sample=sample_indices(len(pairs), 32, 2))
     st = aligner.stats()
-    # the affine / local checkpoint path with the many-pair finish geometry (fin_geom, np > 2 CUs)
+    # the affine / local checkpoint path with the many-pair local finish geometry (fin_geom)
     assert st["checkpoint"] == 1 and st["local"] == 1 and st["tagged"] == 0, st
-    assert (st["fin_waves"], st["fin_slots"]) == (2, 3), st
+    assert (st["fin_waves"], st["fin_slots"]) == (1, 2), st   # local: one wave, two slots
     assert st["npairs"] == 1024
     assert all(r.status == 0 for r in res)
 
