@@ -501,7 +501,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   const size_t np = std::max<size_t>(ncomp, 1);
   const int NC = (int)(maxn2 / 64 + 2);
   double best = 1e300;
-  struct Cand { double T; int R, W, wps, row; };
+  struct Cand { double T; int R, W, wps, row, wavesCu; };
   std::vector<Cand> cands;
   std::vector<int> start, end, diff;
   // relax: no candidate leaves room for a finish workgroup beside the DP's (big alphabets: both
@@ -606,7 +606,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
         T = (h->depth > 1 && !manyAck) ? std::max(T, Tf) + 0.2 * std::min(T, Tf) : T + Tf;
       }
       const int wpsAll = wps * wg;
-      cands.push_back({T, Rc, Wc, wpsAll, rowc ? 1 : 0});
+      cands.push_back({T, Rc, Wc, wpsAll, rowc ? 1 : 0, wg * Wc});
       best = std::min(best, T);
     }
   }
@@ -614,17 +614,30 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   // pipeline tail the model charges for is filled by the overlapped traceback), then more waves
   // per SIMD, then the estimate
   const Cand* pick = nullptr;
+  const bool manyAckPlan = h->ack && !h->tuneW && np >= 2 * (size_t)h->cus;
   if (std::getenv("BG_PLAN_DEBUG"))
     for (const Cand& c : cands)
       std::fprintf(stderr, "plan R %d W %d wps %d T %.4g\n", c.R, c.W, c.wps, c.T);
   // (the affine / local checkpoint path pays taller strips again in the traceback's
   // recomputation: lowest estimate)
   for (const Cand& c : cands) {
-    if (c.T > best * 1.05) continue;
     if (h->ack) {
+      // many pairs: within 8 % of the best estimate, the most DP waves resident per CU (the
+      // model undervalues occupancy there: C5, R = 2, W = 2 keeps 14 waves per CU against 12 for
+      // W = 4 and runs 2 753 against 2 576 GCUPS at an estimate 7 % higher; C2's W = 4 holds the
+      // most waves and the lowest estimate); otherwise the lowest estimate
+      // (W = 1 excluded: one wave per pair hands every strip's row through HBM and rebuilds the
+      // strip prologue alone, which the phase model does not see: C5 at R = 2, W = 1 runs its DP in
+      // 8.7 ms against 5.9 for W = 2)
+      if (manyAckPlan && c.W >= 2 && c.T <= best * 1.08) {
+        if (!pick || c.wavesCu > pick->wavesCu || (c.wavesCu == pick->wavesCu && c.T < pick->T)) pick = &c;
+        continue;
+      }
+      if (c.T > best * 1.05) continue;
       if (!pick || c.T < pick->T) pick = &c;
       continue;
     }
+    if (c.T > best * 1.05) continue;
     if (!pick || c.R > pick->R || (c.R == pick->R && (c.wps > pick->wps || (c.wps == pick->wps && c.T < pick->T))))
       pick = &c;
   }
