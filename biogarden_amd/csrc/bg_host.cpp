@@ -385,8 +385,10 @@ static int pipeline_phases(int S, int gw, int NC, int lag = 2) {
 // per strip and at most the CU count in all, so every group is resident at once.  R minimises
 // the slowest pair's pipeline: phases * 64 steps * the lone-wave step latency.  Measured on C3
 // (BG_DP_TIMING, conveyor step): ~48 + 10R cycles per step (the R-long v_max3 chain of a step
-// plus its DPP and two LDS reads) and a strip starting ~3 chunks after the one above (two for
-// the anti-diagonal skew and the block, one for the hand-off): R = 4-5 beats R = 2 and R = 8.
+// plus its DPP and two LDS reads), and an effective ~5 chunks per strip: a strip starts ~3.3
+// chunks after the one above (two for the anti-diagonal skew and the block, the rest hand-off),
+// and every caught-up consumer adds its hand-off latency to the pace of the strips below it.
+// Fitted on C3's DP at R = 2 / 4 / 5 / 8 (12.3 / 10.1 / 9.8 / 10.3 ms): R = 5.
 static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t npairs, int* Rout,
                       int* Wout) {
   std::vector<size_t> comp;
@@ -415,7 +417,7 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
       int G = std::max(1, std::min((int)share, (S + W - 1) / W));
       groups[p] = G;
       const int NC = (int)(n2[p] / 64 + 2);
-      T = std::max(T, (double)pipeline_phases(S, G * W, NC, 3) * 64.0 * (48.0 + 10.0 * Rc));
+      T = std::max(T, (double)pipeline_phases(S, G * W, NC, 5) * 64.0 * (48.0 + 10.0 * Rc));
     }
     if (T < best) { best = T; bestR = Rc; bestGroups = groups; }
   }
