@@ -38,3 +38,30 @@ def test_wide_edges(aligner, oracle, R, mode, a, b):
         assert st["wide"] == 1 and st["checkpoint"] == 1 and st["R"] == R, st
     finally:
         aligner.set_tuning(0, 0)
+
+
+@pytest.mark.parametrize("depth", [2, 3])
+def test_wide_repeated_executes_alternating_traceback_streams(oracle, depth):
+    """A WIDE batch executed back to back: its tracebacks alternate between two HIP streams and
+    overlap each other (bg_batch_execute), each reading its own arena slot; the fetched result of
+    the last execute must still be the reference's, for every pipeline depth."""
+    from biogarden_amd import _native
+    rng = random.Random(depth)
+    pairs = []
+    for n1, n2 in ((9000, 8800), (4200, 300), (6000, 6100)):
+        s1 = rand_seq(rng, n1, DNA)
+        pairs.append((s1, mutate(rng, s1, DNA, 0.2)[:n2]))
+    h = _native.Handle(0)
+    try:
+        h.set_pipeline(depth)
+        h.prepare("semiglobal", pairs, _native.builtin_scoring(_native.BG_BLOSUM62), -1, -2)
+        assert h.stats()["wide"] == 1
+        for _ in range(5):
+            h.execute()
+        got = h.fetch()
+        for (s1, s2), r in zip(pairs, got):
+            st, sc, o1, o2 = oracle.align("semiglobal", s1, s2, "blosum62", -1, -2, exact=True)
+            assert st == 0 and r["status"] in (0, 4)
+            assert (r["score"], r["aligned1"], r["aligned2"]) == (sc, o1, o2)
+    finally:
+        h.close()
