@@ -275,7 +275,7 @@ extern "C" const char* bg_status_string(int s) {
     case BG_E_IO: return "cannot open file";
     case BG_E_FORMAT: return "Expected > at record start.";
     case BG_E_NO_BATCH: return "no prepared batch";
-    case BG_E_ALPHABET: return "more than 32 symbols with scores beyond the 8-bit-code kernels";
+    case BG_E_ALPHABET: return "more than ~150 symbols with scores beyond int16";
     default: return "unknown";
   }
 }
@@ -562,6 +562,11 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
           wg = 1;
         }
       }
+      if (!h->tag && !h->ack && !h->dna) {
+        // mask kernel, LDS profiles: lut, the 32 x 32 table, then per wave K x 64 lanes x WPE
+        const size_t wpe = h->p32 ? (size_t)Rc : (size_t)(Rc + 1) / 2;
+        if (256 + (h->p32 ? 4096 : 2048) + (size_t)h->kdim * 64 * wpe * 4 + 64 > 160 * 1024) continue;
+      }
       if (h->ack) {
         const size_t ldsCu = 160 * 1024 > finLdsRes ? 160 * 1024 - finLdsRes : 0;
         const size_t one = bg_dp_aff_head_bytes() + (size_t)Wc * bg_dp_aff_wave_lds_bytes(Rc, h->kdim);
@@ -842,9 +847,9 @@ plan_again:
         if (v < -128 || v > 127) ackOK = false;
       }
   h->ack = (ackOK && !ckLimit) ? 1 : 0;
-  // more than 32 symbols in the batch: only the score-only affine-family kernels index their
-  // profile by a code of up to 8 bits (the mask-trace kernel's tables are 32 x 32)
-  if (K > 32 && !h->ack) return BG_E_ALPHABET;
+  // more than 32 symbols in the batch off the score-only affine family: the mask-trace kernel
+  // reads its K x K table (row stride pstride) from HBM while it builds the per-lane profiles,
+  // and the planner keeps one wave's K x 64 profile within the CU's LDS (R <= 2 at K = 256)
 
   // ---- geometry: rows per lane R, waves per workgroup W (one workgroup per pair, or a group
   // of workgroups per pair in the tagged kernel's WIDE mode)
@@ -893,6 +898,9 @@ plan_again:
         if (lds + 64 <= 160 * 1024 || W == 1) break;
         --W;
       }
+      // one wave's K x 64 int32 profile beyond the CU's LDS: more than ~150 symbols with scores
+      // beyond int16 (the only case left without a kernel)
+      if (lds + 64 > 160 * 1024) return BG_E_ALPHABET;
     }
     h->progOff = (int)lds;   // 16 per-wave progress counters follow
     lds += 64;
@@ -980,7 +988,7 @@ plan_again:
   // ---- device memory
   if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->codes1.ensure(o1 + 16) ||
       !h->codes2.ensure(o2 + 16) || !h->lut.ensure(256) ||
-      !h->prof.ensure(std::max<size_t>(4096, (size_t)h->pstride * h->pstride * 2 + 64)) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
+      !h->prof.ensure(std::max<size_t>(4096, (size_t)h->pstride * h->pstride * 4 + 64)) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
       !h->wgmapBuf.ensure(sizeof(int2) * (h->wgmap.size() + 1)) ||
       !h->gprogBuf.ensure(4 * ((size_t)h->progWords + 1)))
     return BG_E_NOMEM;
@@ -1003,7 +1011,7 @@ plan_again:
     const int d = (c < KS && dense[c] >= 0) ? dense[c] : 0;
     lut[x] = (uint8_t)((h->dna && !h->ack) ? d * 8 : d);
   }
-  std::vector<int32_t> prof(std::max<size_t>(1024, ((size_t)h->pstride * h->pstride + 1) / 2), 0);
+  std::vector<int32_t> prof(std::max<size_t>(1024, (size_t)h->pstride * h->pstride), 0);
   if (h->ack) {
     int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
     const int sub = mode == BG_LOCAL ? a : a + b;
@@ -1042,12 +1050,12 @@ plan_again:
     for (int q = 0; q < KS; ++q)
       for (int c = 0; c < KS; ++c)
         if (dense[q] >= 0 && dense[c] >= 0)
-          prof[dense[q] * 32 + dense[c]] = (int32_t)((uint32_t)S.at(q, c) - (uint32_t)a);
+          prof[dense[q] * h->pstride + dense[c]] = (int32_t)((uint32_t)S.at(q, c) - (uint32_t)a);
   } else {
     int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
     for (int q = 0; q < KS; ++q)
       for (int c = 0; c < KS; ++c)
-        if (dense[q] >= 0 && dense[c] >= 0) t16[dense[q] * 32 + dense[c]] = (int16_t)(S.at(q, c) - a);
+        if (dense[q] >= 0 && dense[c] >= 0) t16[dense[q] * h->pstride + dense[c]] = (int16_t)(S.at(q, c) - a);
   }
   st1[o1] = st2[o2] = 0;
   std::memcpy(st2 + o2 + 16, lut, 256);
@@ -1495,7 +1503,7 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
 
 // ------------------------------------------------------------------ edit distance, LCS
 // Both run on the aligner's hot path with a byte-equality scoring over the bytes the batch holds
-// (at most 32 distinct, else BG_E_ALPHABET):
+// (any of the 256):
 //   analysis::seq::edit_distance (src/analysis/seq.rs:105-130) = -(global score) with S = 0 / -1
 //     and a = b = -1 (the Levenshtein recurrence is the linear-gap global DP), score only;
 //   processing::patterns::longest_common_subsequence (src/processing/patterns.rs:82-118) = the

@@ -247,13 +247,20 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
     if (A.codes_in_lds)
       for (int x = threadIdx.x; x < Pp.n2; x += blockDim.x) sCodes[x] = g[x];
   }
+  // the batch's dense table: up to 32 codes staged in LDS (row stride 32); a wider alphabet (up
+  // to 256 codes, row stride A.pstride) is read from HBM/L2 while the per-lane profiles are built
+  const bool wideTab = A.kdim > 32;
   if constexpr (!DNA && P32) {
-    for (int x = threadIdx.x; x < 1024; x += blockDim.x) sTab32[x] = A.profile[x];
+    if (!wideTab)
+      for (int x = threadIdx.x; x < 1024; x += blockDim.x) sTab32[x] = A.profile[x];
   } else if constexpr (!DNA) {
     const int16_t* g = reinterpret_cast<const int16_t*>(A.profile);
-    for (int x = threadIdx.x; x < 1024; x += blockDim.x) sTab[x] = g[x];
+    if (!wideTab)
+      for (int x = threadIdx.x; x < 1024; x += blockDim.x) sTab[x] = g[x];
   }
   __syncthreads();
+  const int16_t* gTab16 = reinterpret_cast<const int16_t*>(A.profile);
+  const int tabStride = wideTab ? A.pstride : 32;
 
   const BgPair P = A.pairs[blockIdx.x];                        // by value: scalar loads, once
   const int n1 = P.n1, n2 = P.n2, nst = P.nstrips, NC = P.nc;
@@ -316,7 +323,8 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
         for (int k = 0; k < R; ++k) {
           const int i = C.rowbase + k + 1;
           const int qq = (i <= n1) ? c1[i - 1] : 0;
-          ldsProf[(cd * BG_WAVE + lane) * R + k] = sTab32[qq * 32 + cd];
+          ldsProf[(cd * BG_WAVE + lane) * R + k] =
+              wideTab ? A.profile[qq * tabStride + cd] : sTab32[qq * 32 + cd];
         }
       }
     } else if constexpr (!DNA) {
@@ -332,7 +340,8 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
             if (k < R) {
               const int i = C.rowbase + k + 1;
               const int qq = (i <= n1) ? c1[i - 1] : 0;
-              v |= ((int)(uint16_t)sTab[qq * 32 + cd]) << (16 * hh);
+              const int16_t t = wideTab ? gTab16[qq * tabStride + cd] : sTab[qq * 32 + cd];
+              v |= ((int)(uint16_t)t) << (16 * hh);
             }
           }
           ldsProf[(cd * BG_WAVE + lane) * WPE + q2] = v;

@@ -60,7 +60,7 @@ enum {
   BG_E_NOMEM = -3,      /* device or host allocation failed */
   BG_E_SCORE_RANGE = -4,/* LCS only: lengths beyond its value frame (scores beyond int16 run the int32-profile kernel) */
   BG_E_NO_BATCH = -5,   /* bg_batch_execute/fetch without a prepared batch */
-  BG_E_ALPHABET = -6,   /* more than 32 symbols in a batch whose scores the 8-bit-code kernels cannot take */
+  BG_E_ALPHABET = -6,   /* more than ~150 symbols in a batch whose scores leave int16 */
   BG_E_IO = -7,         /* bg_fasta_open: the file cannot be opened */
   BG_E_FORMAT = -8      /* bg_fasta_next_batch: "Expected > at record start." (fasta.rs:104-109) */
 };
@@ -122,8 +122,10 @@ int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const uint8_t* cons
 /* bg_batch_prepare with a score table of up to 256 codes (the reference's closure over any
  * bytes, score.rs:38-41 / A.8): code[byte] < k selects row / column of table (k x k, row = seq1
  * code), code[byte] >= k marks a byte the closure panics on (status BG_UNSCORABLE).  Batches
- * using more than 32 codes run on the score-only affine-family kernels; BG_E_ALPHABET if their
- * value range rules them out (scores minus twice the open penalty beyond int8). */
+ * using more than 32 codes run on the score-only affine-family kernels when their values fit
+ * int8 (scores minus the open and extend penalties), otherwise on the mask-trace kernel reading
+ * its k x k table from HBM; BG_E_ALPHABET only when one wave's k x 64 int32 profile exceeds the
+ * CU's LDS (more than ~150 codes with scores beyond int16). */
 int bg_batch_prepare_table(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
                            const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                            const uint16_t* code, int32_t k, const int32_t* table, int32_t a,

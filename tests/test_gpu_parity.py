@@ -131,6 +131,40 @@ def test_custom_closure_beyond_int16(aligner, oracle, mode, a, b):
     assert st["checkpoint"] == 0 and st["tagged"] == 0 and st["R"] == 4, st
 
 
+@pytest.mark.parametrize("mode,a,b,nsym,big", [("global", -11, -1, 70, 900), ("local", -300, -300, 70, 900),
+                                                ("semiglobal", -5, -9, 200, 900), ("fitting", -40, -3, 256, 900),
+                                                ("overlap", -4, -6, 90, 40000), ("global", -30000, -2, 120, 40000)])
+def test_wide_alphabet_beyond_int8(aligner, oracle, mode, a, b, nsym, big):
+    """More than 32 symbols with scores the score-only int8 kernels cannot take (the reference's
+    closure is any i32 over any bytes, score.rs:38-41): the mask-trace kernel, its k x k table
+    read from HBM (int16 entries, or int32 when S - a leaves int16), bit-exact with the oracle."""
+    rng = random.Random(nsym * 7 + big - a)
+    alpha = bytes(range(256 - nsym, 256))
+
+    def fn(x, y):
+        return big if x == y else -(big // 3) - 3 * ((x * 7 + y) % 11)
+    pairs = []
+    for n1, n2 in ((180, 170), (600, 900), (64, 65), (1, 9), (1300, 1200)):
+        s1 = rand_seq(rng, n1, alpha)
+        s2 = mutate(rng, s1, alpha, 0.2)[:n2]
+        if mode == "fitting" and len(s2) > len(s1):
+            s2 = s2[:len(s1)]
+        pairs.append((s1, s2))
+    res = aligner.align_batch(mode, pairs, fn, a, b)
+    sc = oracle.wide_scoring(fn, alpha)
+    matched = 0
+    for (s1, s2), r in zip(pairs, res):
+        st, score, o1, o2 = oracle.align(mode, s1, s2, sc, a, b, exact=True)
+        if st != 0:                      # the reference panics (traceback underflow): so do we
+            assert r.status == st, (mode, len(s1), len(s2), st, r.status)
+            continue
+        assert r.status in (0, 4) and tuple(r[:3]) == (score, o1, o2), (mode, len(s1), len(s2))
+        matched += 1
+    assert matched >= 2
+    st = aligner.stats()
+    assert st["checkpoint"] == 0 and st["tagged"] == 0 and st["R"] == 4, st
+
+
 def test_closure_panics_only_where_reached(aligner, oracle):
     """A closure that panics on one (byte1, byte2) makes exactly the pairs whose DP evaluates
     it unscorable (status 3); the other pairs of the batch align normally (A.8)."""
