@@ -153,8 +153,9 @@ __global__ __launch_bounds__(1024) void bg_dp_aff_kernel(BgDpArgs A) {
         if (c < nblk) {
           const int need = ((s - 1) / W) * nblk + c + 1;
           const int pw = (s - 1) % W;
+          int np = 0;
           while (__hip_atomic_load(sProg + pw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-            __builtin_amdgcn_s_sleep(1);
+            poll_backoff(np);
         }
         if (mailIn) {
           C.bIn = prevMail + (seq % kAffMailSlots) * 64;
@@ -167,8 +168,9 @@ __global__ __launch_bounds__(1024) void bg_dp_aff_kernel(BgDpArgs A) {
       C.mail = nullptr;
       if (mailOut && c >= 1 && c - 1 < nblk) {
         const int needC = seq - kAffMailSlots;
+        int np = 0;
         while (__hip_atomic_load(sCons + w + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < needC)
-          __builtin_amdgcn_s_sleep(1);
+          poll_backoff(np);
         C.mail = mailbox + ((seq - 1) % kAffMailSlots) * 64;
       }
       // checkpoint: the lane's state before this chunk

@@ -13,6 +13,27 @@ namespace bgk {
 
 constexpr int kNegInf = INT32_MIN;  // i32::MIN: x/y buffers' initial value (aligner.rs:49-50)
 
+// Polling an LDS progress counter on the many-wave paths.  The first BG_POLL_FAST polls of a
+// wait sleep 64 cycles (a steady-state wait ends within a few); later ones BG_POLL_LONG x 64, so
+// a wave parked for a long wait (the strip pipeline's fill: the wave of strip s starts ~2s
+// chunks after strip 0) stops taking issue slots from the computing waves of its SIMD.
+// tools/poll_ab.sh, same box: LONG = 1 (every poll 64 cycles) metric 10 100-10 190 / MA 4 630-4 650
+// GCUPS; 8: 10 350 / 4 776; 32: 10 375-10 405 / 4 777-4 783; 127: 10 287 / 4 766; FAST 2-32 alike.
+#ifndef BG_POLL_LONG
+#define BG_POLL_LONG 32
+#endif
+#ifndef BG_POLL_FAST
+#define BG_POLL_FAST 8
+#endif
+__device__ __forceinline__ void poll_backoff(int& n) {
+  if constexpr (BG_POLL_LONG > 1) {
+    if (n < BG_POLL_FAST) { __builtin_amdgcn_s_sleep(1); ++n; }
+    else __builtin_amdgcn_s_sleep(BG_POLL_LONG);
+  } else {
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 __device__ __forceinline__ int dpp_shr1(int old, int src) {
   // v_mov_b32_dpp wave_shr:1 — lane r receives lane r-1; lane 0 keeps `old`.
   return __builtin_amdgcn_update_dpp(old, src, 0x138, 0xf, 0xf, false);

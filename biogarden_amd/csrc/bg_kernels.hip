@@ -366,8 +366,9 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
         if (c < nblk) {                                        // block c of strip s-1
           const int need = ((s - 1) / W) * nblk + c + 1;
           const int pw = (s - 1) % W;
+          int np = 0;
           while (__hip_atomic_load(sProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-            __builtin_amdgcn_s_sleep(1);
+            poll_backoff(np);
         }
         const int32_t* src = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb;
         bM = load_agent(src);

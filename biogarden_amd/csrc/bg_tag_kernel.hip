@@ -73,9 +73,9 @@ __device__ __forceinline__ void wide_poll_pause() {
   if constexpr (BG_WIDE_SLEEP > 0) __builtin_amdgcn_s_sleep(BG_WIDE_SLEEP);
 }
 template <bool WIDE>
-__device__ __forceinline__ void poll_pause() {
+__device__ __forceinline__ void poll_pause(int& n) {
   if constexpr (WIDE) wide_poll_pause();
-  else __builtin_amdgcn_s_sleep(1);
+  else poll_backoff(n);
 }
 
 template <int R>
@@ -285,8 +285,9 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
             while ((int)__hip_atomic_load(gProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
               wide_poll_pause();
           } else {
+            int np = 0;
             while (__hip_atomic_load(sProg + pw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-              poll_pause<WIDE>();
+              poll_pause<WIDE>(np);
           }
         }
         if (mailIn && conv) {
@@ -305,8 +306,9 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       C.mail = nullptr;
       if (mailOut && c >= 1 && c - 1 < nblk) {
         const int needC = seq - kMailSlots;                      // consumer chunks finished
+        int np = 0;
         while (__hip_atomic_load(sCons + w + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < needC)
-          poll_pause<WIDE>();
+          poll_pause<WIDE>(np);
         C.mail = mailbox + ((seq - 1) % kMailSlots) * 64;
       }
       if (dbgOn) tWait += __builtin_amdgcn_s_memtime() - tw0;
