@@ -274,6 +274,9 @@ def main():
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host timing")
     ap.add_argument("--h2h-handles", type=int, default=4)
+    ap.add_argument("--h2h-rounds", type=int, default=24,
+                    help="timed batches of the host-to-host leg (the stream's fill and drain, "
+                         "~one batch's latency, spread over them)")
     args = ap.parse_args()
 
     import torch
@@ -372,7 +375,8 @@ def main():
     h2h = None
     if not args.no_h2h:
         h2h = host_to_host(pairs, args.mode, args.open, args.extend, local_rank,
-                           pipeline=args.pipeline, handles=args.h2h_handles)
+                           pipeline=args.pipeline, handles=args.h2h_handles,
+                           rounds=args.h2h_rounds)
 
     if rank != 0:
         h.close()
