@@ -232,6 +232,12 @@ inline int32_t unit(const uint8_t& a, const uint8_t& b) { return detail::lookup(
 struct Tabulated {
   bg_scoring sc;
   std::set<std::pair<uint8_t, uint8_t>> panics;
+  // more than 32 distinct bytes: the k x k form of bg_batch_prepare_table (code[byte] >= k:
+  // a byte the closure is never evaluated on, status BG_UNSCORABLE if a pair's DP reaches it)
+  bool wide = false;
+  std::vector<uint16_t> code;
+  int32_t k = 0;
+  std::vector<int32_t> table;
 };
 
 using PairRef = std::pair<const std::vector<uint8_t>*, const std::vector<uint8_t>*>;
@@ -251,7 +257,23 @@ inline Tabulated tabulate(const ScoreFn& fn, const std::vector<PairRef>& pairs) 
   }
   std::set<uint8_t> syms(xs);
   syms.insert(ys.begin(), ys.end());
-  if (syms.size() > 32) throw DeviceError(BG_E_ALPHABET);
+  if (syms.size() > 32) {
+    t.wide = true;
+    t.k = (int32_t)syms.size();
+    t.code.assign(256, 0xFFFF);
+    int c = 0;
+    for (uint8_t x : syms) t.code[x] = (uint16_t)c++;
+    t.table.assign((size_t)t.k * t.k, 0);
+    for (uint8_t x : xs)
+      for (uint8_t y : ys) {
+        try {
+          t.table[(size_t)t.code[x] * t.k + t.code[y]] = fn(x, y);
+        } catch (...) {
+          t.panics.insert({x, y});
+        }
+      }
+    return t;
+  }
   std::memset(&t.sc, 0, sizeof(t.sc));
   std::memset(t.sc.code, 0xFF, sizeof(t.sc.code));
   t.sc.alphabet_size = (int32_t)syms.size();
@@ -348,8 +370,15 @@ class SequenceAligner {
     const bg_scoring& sc = tab.sc;
     std::vector<bg_pair_result> res(n ? n : 1);
     std::vector<uint8_t> o1(cap ? cap : 1), o2(cap ? cap : 1);
-    check(bg_align_batch(h_, mode, n, p1.data(), n1.data(), p2.data(), n2.data(), &sc, a, b,
-                         res.data(), o1.data(), o2.data(), cap));
+    if (tab.wide) {
+      check(bg_batch_prepare_table(h_, mode, n, p1.data(), n1.data(), p2.data(), n2.data(),
+                                   tab.code.data(), tab.k, tab.table.data(), a, b));
+      check(bg_batch_execute(h_));
+      check(bg_batch_fetch(h_, res.data(), o1.data(), o2.data(), cap));
+    } else {
+      check(bg_align_batch(h_, mode, n, p1.data(), n1.data(), p2.data(), n2.data(), &sc, a, b,
+                           res.data(), o1.data(), o2.data(), cap));
+    }
     std::vector<PairAlignment> out(n);
     for (size_t i = 0; i < n; ++i) {
       const bg_pair_result& r = res[i];

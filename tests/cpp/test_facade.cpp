@@ -67,6 +67,14 @@ int main(int argc, char** argv) {
     CHECK(c.sc.alphabet_size == 4 && c.panics.size() == 1);
     CHECK(c.sc.table[c.sc.code['C'] * 32 + c.sc.code['G']] == -2);
     CHECK(score::pair_panics(c, s1, s2) && !score::pair_panics(c, s1, s3));
+    // more than 32 distinct bytes: the k x k form for bg_batch_prepare_table
+    std::vector<uint8_t> w1, w2{'!'};
+    for (int i = 0; i < 40; ++i) w1.push_back((uint8_t)(100 + i));
+    std::vector<score::PairRef> vw{{&w1, &w2}};
+    score::Tabulated wt = score::tabulate(f, vw);
+    CHECK(wt.wide && wt.k == 41 && wt.code.size() == 256 && wt.table.size() == 41u * 41u);
+    CHECK(wt.code['!'] == 0 && wt.code[100] == 1 && wt.code['A'] == 0xFFFF);
+    CHECK(wt.table[(size_t)wt.code[100] * wt.k + wt.code['!']] == -2);
   }
 
   // Result / errors

@@ -59,6 +59,23 @@ int main(int argc, char** argv) {
     std::printf("lcs %s scs %s\n", lok ? "ok" : "MISMATCH", sok ? "ok" : "MISMATCH");
     fails += !lok + !sok;
   }
+  // a closure over more than 32 distinct bytes (score.rs:38-41 takes any &dyn Fn): the facade
+  // tabulates it k x k for bg_batch_prepare_table.  40 distinct bytes, seq2 = seq1 less byte 17:
+  // the one optimal global alignment opens one gap there (score 5 * 39 + a)
+  {
+    std::vector<uint8_t> x;
+    for (int i = 0; i < 40; ++i) x.push_back((uint8_t)(200 + i));
+    std::vector<uint8_t> y(x);
+    y.erase(y.begin() + 17);
+    score::ScoreFn f = [](const uint8_t& p, const uint8_t& q) -> int32_t { return p == q ? 5 : -4; };
+    auto r = aligner.global_alignment(ds::Sequence(x), ds::Sequence(y), f, -11, -1);
+    const auto& [sc, a1, a2] = r.unwrap();
+    std::vector<uint8_t> gy(y);
+    gy.insert(gy.begin() + 17, (uint8_t)'-');
+    const bool wok = sc == 5 * 39 - 11 && a1 == ds::Sequence(x) && a2 == ds::Sequence(gy);
+    std::printf("wide alphabet score %d (expect %d) %s\n", sc, 5 * 39 - 11, wok ? "ok" : "MISMATCH");
+    fails += !wok;
+  }
   std::printf("%s\n", fails ? "FAILED" : "integration ok");
   return fails ? 1 : 0;
 }
