@@ -3,8 +3,10 @@
 
     python tools/configs.py [C2 C3 C4 C5 ...] [--steps K] [--check N]
 
-C4 and C5 run the share of one GPU out of 8 (the batch is sharded over ranks, weak per rank).
-Inputs are synthetic as §8(d) describes (uniform DNA / protein, 2 % substituted reads).
+C4 and C5 are one batch over 8 GPUs: the whole job is generated
+(tools/workloads.py) and LPT-sharded by cells over --world ranks (biogarden_amd.shard.lpt_shards,
+the multi-GPU path's partition); this process runs --rank's shard.  Inputs are synthetic as
+§8(d) describes (uniform DNA / protein, 2 % substituted reads).
 --check N compares the first N pairs' scores against the CPU oracle (slow for big pairs).
 """
 import argparse
@@ -26,28 +28,21 @@ def rand_seq(rng, alpha, n):
     return alpha[rng.integers(0, len(alpha), n)].tobytes()
 
 
-def config(name, rng):
+def config(name, rng, rank=0, world=8):
     if name == "C2":      # 1024 x (1000 x 1000) local DNA, blosum62, -11/-1
         pairs = [(rand_seq(rng, DNA, 1000), rand_seq(rng, DNA, 1000)) for _ in range(1024)]
         return "local", pairs, -11, -1
     if name == "C3":      # 1 x (100 000 x 100 000) semiglobal, blosum62, -1/-2
         return "semiglobal", [(rand_seq(rng, DNA, 100000), rand_seq(rng, DNA, 100000))], -1, -2
-    if name == "C4":      # 65 536 reads (150 bp, 2 % substitutions) vs 64 refs of 10 kbp; 1/8
-        refs = [rand_seq(rng, DNA, 10000) for _ in range(8)]
-        pairs = []
-        for r in refs:
-            ra = np.frombuffer(r, dtype=np.uint8)
-            for _ in range(1024):
-                o = int(rng.integers(0, 10000 - 150))
-                read = ra[o:o + 150].copy()
-                m = rng.random(150) < 0.02
-                read[m] = DNA[rng.integers(0, 4, int(m.sum()))]
-                pairs.append((read.tobytes(), r))
-        return "semiglobal", pairs, -1, -2
-    if name == "C5":      # all-vs-all 256 proteins U[64, 4000], global, blosum62, -11/-1; 1/8
-        prots = [rand_seq(rng, PROT, int(rng.integers(64, 4001))) for _ in range(256)]
-        allp = [(prots[i], prots[j]) for i in range(256) for j in range(i + 1, 256)]
-        return "global", allp[0::8], -11, -1
+    if name in ("C4", "C5"):  # one batch over `world` GPUs: this rank's LPT shard of the job
+        from biogarden_amd.shard import lpt_shards
+        from tools import workloads
+        if name == "C4":      # 65 536 reads (150 bp, 2 % substitutions) vs 64 refs of 10 kbp
+            mode, allp, a, b = "semiglobal", workloads.c4_pairs(), -1, -2
+        else:                 # all-vs-all 256 proteins U[64, 4000], global, blosum62, -11/-1
+            mode, allp, a, b = "global", workloads.c5_pairs(), -11, -1
+        shards = lpt_shards([(len(x), len(y)) for x, y in allp], world)
+        return mode, [allp[p] for p in shards[rank]], a, b
     raise ValueError(name)
 
 
@@ -61,6 +56,8 @@ def main():
     ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--kernel-options", type=int, default=7)
     ap.add_argument("--timing", action="store_true", help="finish-kernel cycle breakdown (stderr)")
+    ap.add_argument("--rank", type=int, default=0, help="C4 / C5: the shard this GPU runs")
+    ap.add_argument("--world", type=int, default=8, help="C4 / C5: GPUs the job is sharded over")
     args = ap.parse_args()
     if args.timing:
         os.environ["BG_FINISH_TIMING"] = "1"
@@ -73,7 +70,7 @@ def main():
     sc = _native.builtin_scoring(_native.BG_BLOSUM62)
     for i, name in enumerate(args.configs):
         rng = np.random.default_rng(0xB10A11F0 + int(name[1:]))
-        mode, pairs, a, b = config(name, rng)
+        mode, pairs, a, b = config(name, rng, args.rank, args.world)
         t0 = time.perf_counter()
         h.prepare(mode, pairs, sc, a, b)
         prep = time.perf_counter() - t0
@@ -94,6 +91,8 @@ def main():
                 "dp_ms": round(dp, 3), "finish_ms": round(fin, 3), "prepare_s": round(prep, 3),
                 "R": st["R"], "waves": st["waves"], "affine": st["affine"], "tagged": st["tagged"],
                 "dna": st["dna"], "bad_status": bad}
+        if name in ("C4", "C5"):
+            line["shard"] = "rank %d of %d (LPT by cells)" % (args.rank, args.world)
         if args.check:
             from oracle import refcpu
             k = min(args.check, len(pairs))
