@@ -284,10 +284,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # BG_BENCH_BACKEND=gloo rehearses the N > 1 path on a box with fewer GPUs than ranks (ranks
+    # share devices round-robin, collectives on host tensors); the driver's runs use RCCL
+    backend = os.environ.get("BG_BENCH_BACKEND", "nccl")
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         import torch.distributed as dist
+        local_rank = local_rank % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
 
     from biogarden_amd import _native, shard
 
@@ -299,7 +307,7 @@ def main():
     def max_over_ranks(x):
         if dist is None:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device="cuda")
+        t = torch.tensor([x], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -322,7 +330,7 @@ def main():
     elapsed, dp_ms, fin_ms = timed(h, args.steps, args.warmup, barrier)
     elapsed = max_over_ranks(elapsed)
     if dist is not None:
-        t = torch.tensor([float(cells)], dtype=torch.float64, device="cuda")
+        t = torch.tensor([float(cells)], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t)
         total_cells = float(t.item())
     else:
@@ -339,7 +347,7 @@ def main():
     if dist is not None and not args.no_gather:
         barrier()
         tg = time.perf_counter()
-        packed = shard.gather_packed(local, dist, dst=0)
+        packed = shard.gather_packed(local if coll_dev == "cuda" else local.cpu(), dist, dst=0)
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         if rank == 0:
