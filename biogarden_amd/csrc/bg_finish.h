@@ -9,6 +9,15 @@
 
 #include "bg_aff_common.h"
 #include "bg_dev_util.h"
+
+// idle recompute helpers of the checkpoint traceback (bg_finish_ck): BG_HELP_FAST polls 512
+// cycles apart, then BG_HELP_LONG x 64 cycles apart
+#ifndef BG_HELP_FAST
+#define BG_HELP_FAST 4
+#endif
+#ifndef BG_HELP_LONG
+#define BG_HELP_LONG 8
+#endif
 #include "bg_device.h"
 #include "bg_tag_common.h"
 
@@ -507,6 +516,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       const unsigned e = __hip_atomic_load(&ckMap[ck_map_idx(key >> 16, key & 0xffff)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       return e != 0xFFFFFFFFu && (int)(e >> 4) == key;
     };
+    int idle = 0;
     for (;;) {
       if (__hip_atomic_load(&sh[32], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
       int key = -1, zz = -1;
@@ -574,7 +584,15 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       }
       key = uni(__shfl(key, 0, 64));
       zz = uni(__shfl(zz, 0, 64));
-      if (key < 0) { __builtin_amdgcn_s_sleep(8); continue; }
+      if (key < 0) {
+        // idle: nothing to recompute ahead of the walk.  Each poll takes the lock and scans the
+        // candidates on a SIMD the next execute's DP waves share; after BG_HELP_FAST idle polls
+        // the helper polls BG_HELP_LONG x 64 cycles apart
+        if (idle < BG_HELP_FAST) { __builtin_amdgcn_s_sleep(8); ++idle; }
+        else __builtin_amdgcn_s_sleep(BG_HELP_LONG);
+        continue;
+      }
+      idle = 0;
       recompute_chunk<R>(F, P, key >> 16, key & 0xffff, win + (size_t)zz * kSlotDw,
                          ckArea + wid * ckAreaInts, lane);
       if (F.dbg && lane == 0) __hip_atomic_fetch_add(&sh[37], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
