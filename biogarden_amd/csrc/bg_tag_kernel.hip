@@ -69,12 +69,25 @@ constexpr int kMailSlots = BG_MAIL_SLOTS;   // boundary blocks in flight between
 #ifndef BG_WIDE_SLEEP
 #define BG_WIDE_SLEEP 0
 #endif
-__device__ __forceinline__ void wide_poll_pause() {
+// BG_WIDE_LONG > 0: a wait that outlasts BG_WIDE_FAST spinning polls (the strip pipeline's fill,
+// where the wave of strip s waits ~5s chunks) sleeps BG_WIDE_LONG x 64 cycles between polls, so
+// hundreds of parked waves stop loading progress counters through L2 beside the working strips
+#ifndef BG_WIDE_LONG
+#define BG_WIDE_LONG 0
+#endif
+#ifndef BG_WIDE_FAST
+#define BG_WIDE_FAST 256
+#endif
+__device__ __forceinline__ void wide_poll_pause(int& n) {
+  if constexpr (BG_WIDE_LONG > 0) {
+    if (n < BG_WIDE_FAST) ++n;
+    else __builtin_amdgcn_s_sleep(BG_WIDE_LONG);
+  }
   if constexpr (BG_WIDE_SLEEP > 0) __builtin_amdgcn_s_sleep(BG_WIDE_SLEEP);
 }
 template <bool WIDE>
 __device__ __forceinline__ void poll_pause(int& n) {
-  if constexpr (WIDE) wide_poll_pause();
+  if constexpr (WIDE) wide_poll_pause(n);
   else poll_backoff(n);
 }
 
@@ -228,9 +241,10 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     const int32_t* bndAbove = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + lane;
     int nbV = 0, pollV = 0;
     if (hbmAhead) {
+      int np0 = 0;
       if (0 < nblk)
         while ((int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < needBase + 1)
-          wide_poll_pause();
+          wide_poll_pause(np0);
       nbV = load_agent(bndAbove);
       pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -269,8 +283,9 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         }
         if (c + 1 < NC) {
           if (c + 1 < nblk) {
+            int np1 = 0;
             while (pollV < needBase + c + 2) {
-              wide_poll_pause();
+              wide_poll_pause(np1);
               pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           }
@@ -282,8 +297,9 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
           const int need = ((s - 1) / GW) * nblk + c + 1;
           const int pw = mailIn ? prevW : (s - 1) % GW;
           if (WIDE && !mailIn) {
+            int np2 = 0;
             while ((int)__hip_atomic_load(gProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
-              wide_poll_pause();
+              wide_poll_pause(np2);
           } else {
             int np = 0;
             while (__hip_atomic_load(sProg + pw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
