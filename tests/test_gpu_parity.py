@@ -144,7 +144,8 @@ def test_wide_alphabet_beyond_int8(aligner, oracle, mode, a, b, nsym, big):
     def fn(x, y):
         return big if x == y else -(big // 3) - 3 * ((x * 7 + y) % 11)
     pairs = []
-    for n1, n2 in ((180, 170), (600, 900), (64, 65), (1, 9), (1300, 1200)):
+    # 3000 rows: 12 strips at R = 4, through HBM boundary rows when one wave fills the LDS
+    for n1, n2 in ((180, 170), (600, 900), (64, 65), (1, 9), (1300, 1200), (3000, 2800)):
         s1 = rand_seq(rng, n1, alpha)
         s2 = mutate(rng, s1, alpha, 0.2)[:n2]
         if mode == "fitting" and len(s2) > len(s1):
