@@ -168,8 +168,8 @@ struct bg_aligner {
   hipStream_t stream3 = nullptr;   // WIDE batches: every other execute's traceback (see execute)
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
   DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
-  Slot slot[3];
-  int depth = 3;                   // pipeline depth: arena slots in flight (1..3; 3 lets the
+  Slot slot[4];
+  int depth = 3;                   // pipeline depth: arena slots in flight (1..4; 3 lets the
                                    // traceback of step k overlap the DPs of k+1 and k+2)
   int execCount = 0;
   int lastSlot = 0;
@@ -351,7 +351,7 @@ extern "C" int bg_set_kernel_options(bg_aligner* h, int allow_tagged) {
 }
 
 extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
-  if (!h || depth < 1 || depth > 3) return BG_E_ARG;
+  if (!h || depth < 1 || depth > 4) return BG_E_ARG;
   if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream2) != hipSuccess || hipStreamSynchronize(h->stream3) != hipSuccess)
     return BG_E_HIP;

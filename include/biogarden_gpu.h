@@ -186,7 +186,7 @@ int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes);
 /* Tuning overrides for tests/benchmarks (0 = automatic). */
 int bg_set_tuning(bg_aligner* h, int R, int waves);
 
-/* Pipeline depth 1-3: with 2 or 3 (default) slots of per-execute arenas the end-cell/traceback
+/* Pipeline depth 1-4: with 2 to 4 (default 3) slots of per-execute arenas the end-cell/traceback
  * kernel of execute k overlaps the DP kernel of execute k+1 (two HIP streams); 1 serialises.
  * Takes effect at the next bg_batch_prepare. */
 int bg_set_pipeline(bg_aligner* h, int depth);
