@@ -12,11 +12,15 @@ One step = one pass of the hot path over the batch with the inputs resident in H
 -> end-cell search -> traceback writing both aligned strings (aligner.rs:351-435), three
 pipeline slots (the traceback of step k overlaps the DP of step k+1).  Every rank aligns its own
 256 pairs (weak scaling: the pairs are independent, no data-path collective); after the timed
-region the per-rank packed results are gathered to rank 0 over RCCL (gather_ms).  `--shard`
-instead LPT-shards one batch of 256 pairs over the ranks (strong scaling, §8(d)'s phrasing).
+region the per-rank packed results are gathered to rank 0 over RCCL (gather_ms).  With more than
+one rank the line also carries `strong`: ONE batch of 256 pairs LPT-sharded over the ranks, each
+step ending with the device-side export and the RCCL gather to rank 0 inside the timed wall
+(§8(d)'s wall).  `--shard` makes that form the headline.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+    ... bench.py --config C4|C5    the whole 8-GPU job of SURVEY §8(d) C4 / C5, LPT-sharded over
+                                   the ranks, export + RCCL gather to rank 0 inside every step
 
 Fields beyond the driver's contract:
   roofline        the DP kernel (the dominant one) against §8(d)'s algorithmic bytes
@@ -24,10 +28,13 @@ Fields beyond the driver's contract:
                   HBM peak 8 TB/s; `bound` names the roof that binds (VALU issue) and `valu`
                   its fraction: PMC-measured VALU instructions x 64 lanes / kernel time against
                   256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (MI355X_MICROARCH.md)
+  configs         (N = 1) the other BASELINE configurations on this GPU, each with its value,
+                  step time, DP / traceback kernel times and roofline: C2, C3, and C4 / C5 as
+                  one GPU's LPT share of their 8-GPU jobs
   host_to_host    PCIe-inclusive rate through the streaming API (biogarden_amd.stream): residues
                   uploaded from host buffers, aligned strings downloaded to host buffers, four
                   handles in rotation so batches' uploads and downloads overlap the kernels of
-                  the batches in flight (never `value`)
+                  the batches in flight (never `value`), with the host's time per phase
   cpu_baseline    the oracle (oracle/refcpu.c: the reference's six full matrices, its loop order,
                   one reused aligner per thread) on this host's cores, plus a 1-core rate and C1
 """
@@ -171,20 +178,52 @@ def roofline(st, cells, dp_ms, workload, a, b):
 # ------------------------------------------------------------------ timed runs
 
 
-def timed(h, steps, warmup, barrier):
+def timed(h, steps, warmup, barrier, per_step=None):
+    """K executes between barriers; `per_step` (the export + gather of a sharded job) runs after
+    every execute, inside the timed region."""
     for _ in range(warmup):
         h.execute()
+        if per_step:
+            per_step()
     h.synchronize()
     barrier()
     h.profile_begin()
     t0 = time.perf_counter()
     for _ in range(steps):
         h.execute()
+        if per_step:
+            per_step()
     h.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     dp_ms, fin_ms, _ = h.profile_end()
     return elapsed, dp_ms, fin_ms
+
+
+def gatherer(h, dist, coll_dev):
+    """Per-step §8(e) result path: bg_batch_export packs the last execute's records and strings
+    device-to-device, then one variable-size gather to rank 0 (RCCL over xGMI; gloo rehearsal on
+    host tensors).  Returns a callable -> rank 0: list of per-rank packed bytes."""
+    import torch
+    from biogarden_amd import shard
+    nbytes = h.export_size()
+    local = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda")
+
+    def step():
+        h.export_to(local.data_ptr(), nbytes)
+        src = local[:nbytes]
+        return shard.gather_packed(src if coll_dev == "cuda" else src.cpu(), dist, dst=0)
+    return step
+
+
+def sharded_job(pairs, mode, a, b, world, rank):
+    """LPT shard of one batch (shard.lpt_shards, balanced by cells) with the per-pair scratch
+    dims a single reference aligner would start each call from (shard.call_dims)."""
+    from biogarden_amd import shard
+    sizes = [(len(x), len(y)) for x, y in pairs]
+    shards = shard.lpt_shards(sizes, world)
+    mine = shards[rank]
+    return [pairs[p] for p in mine], shard.shard_call_dims(mode, sizes, a, b, mine), shards
 
 
 def host_to_host(pairs, mode, a, b, device, rounds=8, pipeline=3, handles=4):
@@ -200,16 +239,25 @@ def host_to_host(pairs, mode, a, b, device, rounds=8, pipeline=3, handles=4):
         for _ in range(handles):                       # warm every handle's arenas
             st.submit(pairs)
         st.drain()
+        st.host_timing(reset=True)
         t0 = time.perf_counter()
         done = 0
         for r in range(rounds):
             done += len(st.submit(pairs, tag=r))
         done += len(st.drain())
         secs = time.perf_counter() - t0
+        ht = st.host_timing()
     assert done == rounds
     cells = workloads.cells(pairs)
+    # per batch: the host is one thread through the rotation, so its phases add up to the wall;
+    # `other` is Python, the launches and the waits outside prepare / fetch
+    phases = {k: round(v / rounds, 4) for k, v in ht.items()
+              if k not in ("prepares", "fetches", "host_threads")}
+    phases["other"] = round(secs * 1e3 / rounds - sum(phases.values()), 4)
     return {"gcups": round(cells * rounds / secs / 1e9, 2), "rounds": rounds, "handles": handles,
             "seconds_per_batch": round(secs / rounds, 5),
+            "host_ms_per_batch": phases, "host_threads": int(ht.get("host_threads", 0)),
+            "prepares": int(ht.get("prepares", 0)), "fetches": int(ht.get("fetches", 0)),
             "covers": "biogarden_amd.stream.AlignStream: bg_batch_prepare (validation, pinned "
                       "staging, H2D) + execute + bg_batch_fetch (D2H, aligned strings in host "
                       "buffers), %d handles in rotation" % handles}
@@ -247,6 +295,41 @@ def cpu_section(pairs, gpu_scores, mode, a, b, info, pairs_multi, pairs_one):
     return out
 
 
+def kernel_info(st, pipeline):
+    return {"R": st["R"], "waves": st["waves"], "affine": st["affine"], "tagged": st["tagged"],
+            "checkpoint": st["checkpoint"], "wide": st["wide"], "dna_profile": st["dna"],
+            "pipeline": pipeline, "fin_waves": st["fin_waves"], "fin_slots": st["fin_slots"]}
+
+
+CONFIG_STEPS = {"C2": 12, "C3": 12, "C4": 12, "C5": 8}
+
+
+def config_leg(h, sc, name, barrier, pipeline, steps=None):
+    """One SURVEY §8(d) configuration on this GPU (N = 1): C2 / C3 whole, C4 / C5 as rank 0's
+    LPT share of their 8-GPU jobs (with the whole job's call history for status 4)."""
+    mode, pairs, a, b = workloads.job(name)
+    job_cells = workloads.cells(pairs)
+    share = None
+    if name in ("C4", "C5"):
+        pairs, dims, shards = sharded_job(pairs, mode, a, b, 8, 0)
+        h.set_call_dims(dims)
+        share = "rank 0 of 8 (LPT by cells): %d of %d pairs, %.4g of %.4g cells" % (
+            len(pairs), sum(len(x) for x in shards), workloads.cells(pairs), job_cells)
+    h.prepare(mode, pairs, sc, a, b)
+    st = h.stats()
+    k = steps or CONFIG_STEPS[name]
+    el, dp, fin = timed(h, k, 2, barrier)
+    res = h.fetch_raw()
+    roof = roofline(st, st["cells"], dp, name, a, b)
+    roof["finish_ms"] = round(fin, 4)
+    return {"workload": workloads.DESCRIPTION[name], "pairs": len(pairs), "cells": st["cells"],
+            "share": share, "value": round(st["cells"] * k / el / 1e9, 3), "unit": "GCUPS",
+            "steps": k, "ms_per_step": round(el / k * 1e3, 4), "dp_ms": round(dp, 4),
+            "finish_ms": round(fin, 4), "kernel": kernel_info(st, pipeline), "roofline": roof,
+            "all_status_ok": all(x in (0, 4) for x in res["status"]),
+            "status4": sum(1 for x in res["status"] if x == 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -266,7 +349,13 @@ def main():
                     help="slots: >= 2 lets the traceback of step k overlap the DP of step k+1 "
                          "(two HIP streams); 3 absorbs traceback times that vary around the DP's")
     ap.add_argument("--shard", action="store_true",
-                    help="strong scaling: LPT-shard one batch of --pairs over the ranks")
+                    help="strong scaling as the headline: LPT-shard one batch of --pairs over the "
+                         "ranks, export + gather inside every step")
+    ap.add_argument("--config", choices=["C2", "C3", "C4", "C5"],
+                    help="headline = this whole SURVEY 8(d) job LPT-sharded over the ranks, "
+                         "export + gather to rank 0 inside every step")
+    ap.add_argument("--configs", default="C2,C3,C4,C5",
+                    help="N = 1: configurations timed beside M ('' for none)")
     ap.add_argument("--cpu-pairs", type=int, default=32, help="M pairs for the all-core CPU rate")
     ap.add_argument("--cpu-one-pairs", type=int, default=8, help="M pairs for the 1-core CPU rate")
     ap.add_argument("--no-cpu", action="store_true")
@@ -297,7 +386,7 @@ def main():
         else:
             dist.init_process_group(backend)
 
-    from biogarden_amd import _native, shard
+    from biogarden_amd import _native
 
     def barrier():
         if dist is not None:
@@ -311,52 +400,81 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    def sum_over_ranks(x):
+        if dist is None:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t)
+        return float(t.item())
+
     h = _native.Handle(local_rank)
     if args.R or args.waves:
         h.set_tuning(args.R, args.waves)
     h.set_pipeline(args.pipeline)
-    if args.shard:
-        allpairs = make_pairs(args.pairs, args.len1, args.len2, SEED)
-        shards = shard.lpt_shards([(len(x), len(y)) for x, y in allpairs], world)
-        pairs = [allpairs[p] for p in shards[rank]]
-    else:
-        pairs = make_pairs(args.pairs, args.len1, args.len2, SEED + 1000003 * rank)
     sc = _native.builtin_scoring(_native.BG_BLOSUM62)
 
-    # ---- M: the metric workload
+    if args.config:
+        job_line(args, h, sc, world, rank, dist, coll_dev, barrier, max_over_ranks, sum_over_ranks)
+        return
+
+    # ---- M: the metric workload (own 256 pairs per rank; --shard: one batch sharded)
+    strong_head = args.shard and world > 1
+    if strong_head:
+        pairs, dims, _ = sharded_job(make_pairs(args.pairs, args.len1, args.len2, SEED), args.mode,
+                                     args.open, args.extend, world, rank)
+        h.set_call_dims(dims)
+    else:
+        pairs = make_pairs(args.pairs, args.len1, args.len2, SEED + 1000003 * rank)
     h.prepare(args.mode, pairs, sc, args.open, args.extend)
     st = h.stats()
     cells = st["cells"]
-    elapsed, dp_ms, fin_ms = timed(h, args.steps, args.warmup, barrier)
+    gstep = gatherer(h, dist, coll_dev) if (strong_head and not args.no_gather) else None
+    elapsed, dp_ms, fin_ms = timed(h, args.steps, args.warmup, barrier, gstep)
     elapsed = max_over_ranks(elapsed)
-    if dist is not None:
-        t = torch.tensor([float(cells)], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t)
-        total_cells = float(t.item())
-    else:
-        total_cells = float(cells)
+    total_cells = sum_over_ranks(cells)
     gcups = total_cells * args.steps / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
 
-    # ---- results: RCCL gather of every rank's packed results to rank 0 (after the timed region)
+    # ---- results: RCCL gather of every rank's packed results to rank 0 (after the timed
+    # region for the weak form; the strong form gathered inside every step)
     gather_ms = None
     results0 = None
-    nbytes = h.export_size()
-    local = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
-    h.export_to(local.data_ptr(), nbytes)
     if dist is not None and not args.no_gather:
+        g = gstep or gatherer(h, dist, coll_dev)
         barrier()
         tg = time.perf_counter()
-        packed = shard.gather_packed(local if coll_dev == "cuda" else local.cpu(), dist, dst=0)
+        packed = g()
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         if rank == 0:
             results0 = [_native.decode_export(b) for b in packed]
     else:
-        results0 = [_native.decode_export(local.cpu().numpy().tobytes())]
+        nbytes = h.export_size()
+        local = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda")
+        h.export_to(local.data_ptr(), nbytes)
+        results0 = [_native.decode_export(local[:nbytes].cpu().numpy().tobytes())]
     workload = workload_name(args.mode, args.pairs, args.len1, args.len2, args.open, args.extend)
     roof = roofline(st, cells, dp_ms, workload, args.open, args.extend)
     roof["finish_ms"] = round(fin_ms, 4)
+
+    # ---- strong scaling beside the weak headline (N > 1): one batch of 256 pairs over the ranks
+    strong = None
+    if world > 1 and not args.shard:
+        hs = _native.Handle(local_rank)
+        hs.set_pipeline(args.pipeline)
+        spairs, sdims, _ = sharded_job(make_pairs(args.pairs, args.len1, args.len2, SEED),
+                                       args.mode, args.open, args.extend, world, rank)
+        hs.set_call_dims(sdims)
+        hs.prepare(args.mode, spairs, sc, args.open, args.extend)
+        sst = hs.stats()
+        se, sdp, sfin = timed(hs, args.steps, args.warmup, barrier, gatherer(hs, dist, coll_dev))
+        se = max_over_ranks(se)
+        scells = sum_over_ranks(sst["cells"])
+        strong = {"value": round(scells * args.steps / se / 1e9, 3), "unit": "GCUPS",
+                  "ms_per_step": round(se / args.steps * 1e3, 4), "pairs_total": args.pairs,
+                  "pairs_this_rank": len(spairs), "dp_ms": round(sdp, 4), "finish_ms": round(sfin, 4),
+                  "gather_in_wall": True, "scaling": "strong"}
+        hs.close()
 
     # ---- MA: the same pairs with a genuinely affine gap model (open < extend)
     aff = None
@@ -364,20 +482,24 @@ def main():
         a2, b2 = args.affine_open, args.affine_extend
         h.prepare(args.mode, pairs, sc, a2, b2)
         sta = h.stats()
-        ea, dpa, fina = timed(h, max(2, args.steps // 2), max(1, args.warmup // 2), barrier)
-        ea = max_over_ranks(ea)
         na = max(2, args.steps // 2)
+        ea, dpa, fina = timed(h, na, max(1, args.warmup // 2), barrier)
+        ea = max_over_ranks(ea)
         resa = h.fetch_raw()
         wla = workload_name(args.mode, args.pairs, args.len1, args.len2, a2, b2)
         ra = roofline(sta, sta["cells"], dpa, wla, a2, b2)
         ra["finish_ms"] = round(fina, 4)
-        aff = {"workload": wla, "value": round(total_cells * na / ea / 1e9, 3), "unit": "GCUPS",
-               "steps": na, "ms_per_step": round(ea / na * 1e3, 4),
-               "gap_open": a2, "gap_extend": b2,
-               "kernel": {"R": sta["R"], "waves": sta["waves"], "affine": sta["affine"],
-                          "checkpoint": sta["checkpoint"], "fin_waves": sta["fin_waves"],
-                          "fin_slots": sta["fin_slots"]},
+        aff = {"workload": wla, "value": round(sum_over_ranks(sta["cells"]) * na / ea / 1e9, 3),
+               "unit": "GCUPS", "steps": na, "ms_per_step": round(ea / na * 1e3, 4),
+               "gap_open": a2, "gap_extend": b2, "kernel": kernel_info(sta, args.pipeline),
                "roofline": ra, "all_status_ok": all(s == 0 for s in resa["status"])}
+
+    # ---- the other BASELINE configurations on this GPU (N = 1)
+    cfgs = None
+    if world == 1 and args.configs:
+        cfgs = {}
+        for name in [c for c in args.configs.split(",") if c]:
+            cfgs[name] = config_leg(h, sc, name, barrier, args.pipeline)
 
     # ---- host-to-host rate (not `value`): host buffers in, aligned strings back on the host
     h2h = None
@@ -410,28 +532,78 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "strong" if args.shard else "weak",
+        "scaling": "strong" if strong_head else "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (uniform DNA, numpy PCG64 seed 0x%X%s)" % (
-            SEED, "" if args.shard else " + 1000003*rank"),
+            SEED, "" if strong_head else " + 1000003*rank"),
         "config": {"workload": workload, "pairs_per_gpu": len(pairs), "len1": args.len1,
                    "len2": args.len2, "mode": args.mode, "scoring": "blosum62",
                    "gap_open": args.open, "gap_extend": args.extend,
-                   "kernel": {"R": st["R"], "waves": st["waves"], "affine": st["affine"],
-                              "tagged": st["tagged"], "checkpoint": st["checkpoint"],
-                              "dna_profile": st["dna"], "pipeline": args.pipeline,
-                              "fin_waves": st["fin_waves"], "fin_slots": st["fin_slots"]},
-                   "parallelism": "dp%d (%s)" % (world, "one batch LPT-sharded" if args.shard
+                   "kernel": kernel_info(st, args.pipeline),
+                   "parallelism": "dp%d (%s)" % (world, "one batch LPT-sharded, gather in every "
+                                                 "step" if strong_head
                                                  else "independent pairs per rank")},
         "roofline": roof,
         "cpu_baseline": cpu,
         "affine": aff,
+        "strong": strong,
+        "configs": cfgs,
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         "host_to_host": h2h,
         "all_status_ok": ok_status,
     }
     print(json.dumps(line))
+    h.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def job_line(args, h, sc, world, rank, dist, coll_dev, barrier, max_over_ranks, sum_over_ranks):
+    """--config C2..C5: the whole SURVEY §8(d) job LPT-sharded over the ranks (§8(e)); every
+    step = execute + device export + gather to rank 0 (RCCL), so the wall is §8(d)'s."""
+    import torch
+    from biogarden_amd import _native
+    name = args.config
+    mode, allp, a, b = workloads.job(name)
+    pairs, dims, shards = sharded_job(allp, mode, a, b, world, rank)
+    h.set_call_dims(dims)
+    h.prepare(mode, pairs, sc, a, b)
+    st = h.stats()
+    g = gatherer(h, dist, coll_dev) if dist is not None else None
+    steps = args.steps
+    el, dp, fin = timed(h, steps, args.warmup, barrier, g)
+    el = max_over_ranks(el)
+    total = sum_over_ranks(st["cells"])
+    # the same job without the per-step gather (executes pipelined back to back)
+    el2, _, _ = timed(h, steps, 1, barrier)
+    el2 = max_over_ranks(el2)
+    if g is not None:
+        packed = g()
+    else:
+        nbytes = h.export_size()
+        local = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda")
+        h.export_to(local.data_ptr(), nbytes)
+        packed = [local[:nbytes].cpu().numpy().tobytes()]
+    roof = roofline(st, st["cells"], dp, name, a, b)
+    roof["finish_ms"] = round(fin, 4)
+    if rank == 0:
+        from biogarden_amd import shard
+        merged = shard.merge_shards(shards, [_native.decode_export(x) for x in packed])
+        line = {"metric": "GCUPS (billion DP cells/s), %s, %d MI355X" % (name, world),
+                "value": round(total * steps / el / 1e9, 3), "unit": "GCUPS", "n_gpus": world,
+                "steps": steps, "warmup": args.warmup, "ms_per_step": round(el / steps * 1e3, 4),
+                "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+                "dtype": "int32", "data": "synthetic (tools/workloads.py, seed 0xB10A11F0 + %s)" % name[1:],
+                "config": {"workload": workloads.DESCRIPTION[name], "pairs": len(allp),
+                           "cells": int(total), "kernel": kernel_info(st, args.pipeline),
+                           "parallelism": "dp%d (whole job LPT-sharded by cells, export + "
+                                          "gather to rank 0 in every step)" % world},
+                "pipelined_no_gather": {"value": round(total * steps / el2 / 1e9, 3),
+                                        "ms_per_step": round(el2 / steps * 1e3, 4)},
+                "roofline": roof,
+                "all_status_ok": all(r is not None and r["status"] in (0, 4) for r in merged)}
+        print(json.dumps(line))
     h.close()
     if dist is not None:
         dist.destroy_process_group()

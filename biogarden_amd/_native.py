@@ -21,7 +21,8 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_synchronize", "bg_get_stats", "bg_set_tuning", "bg_status_string",
            "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
            "bg_set_pipeline", "bg_set_kernel_options", "bg_edit_distance_batch",
-           "bg_lcs_batch", "bg_aligner_buffer_size", "bg_aligner_set_buffer_size", "bg_fasta_open",
+           "bg_lcs_batch", "bg_aligner_buffer_size", "bg_aligner_set_buffer_size",
+           "bg_aligner_set_call_dims", "bg_host_timing", "bg_fasta_open",
            "bg_batch_prepare_table", "bg_fasta_next_batch",
            "bg_fasta_close"]
 
@@ -115,6 +116,9 @@ def lib():
     L.bg_aligner_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.c_size_t)]
     L.bg_aligner_set_buffer_size.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t]
+    L.bg_aligner_set_call_dims.argtypes = [ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_uint64)]
     L.bg_set_tuning.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     L.bg_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.bg_set_kernel_options.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -124,6 +128,8 @@ def lib():
     L.bg_profile_begin.argtypes = [ctypes.c_void_p]
     L.bg_profile_end.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    L.bg_host_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
+                                 ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.bg_batch_export.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.POINTER(ctypes.c_size_t)]
     pair_args = [ctypes.c_void_p, ctypes.c_size_t,
@@ -338,9 +344,30 @@ class Handle:
         check(lib().bg_aligner_buffer_size(self._p, ctypes.byref(r), ctypes.byref(c)))
         return r.value, c.value
 
-
     def set_buffer_size(self, rows, cols):
         check(lib().bg_aligner_set_buffer_size(self._p, rows, cols))
+
+    def set_call_dims(self, dims):
+        """Per-pair scratch dims the next prepared batch's calls start from (a shard of a larger
+        batch: shard.call_dims); None or [] clears."""
+        n = len(dims) if dims else 0
+        rows = (ctypes.c_uint64 * max(n, 1))(*[d[0] for d in dims or []])
+        cols = (ctypes.c_uint64 * max(n, 1))(*[d[1] for d in dims or []])
+        check(lib().bg_aligner_set_call_dims(self._p, n, rows, cols))
+
+    HOST_PHASES = ("wait_previous", "validate_stage", "plan", "alloc", "upload", "fetch_wait",
+                   "fetch_d2h", "fetch_unpack")
+
+    def host_timing(self, reset=False):
+        """Accumulated host-side ms per phase of prepare / fetch (bg_host_timing), plus the call
+        counts and the host threads of the byte passes."""
+        ms = (ctypes.c_double * 8)()
+        calls = (ctypes.c_uint64 * 3)()
+        check(lib().bg_host_timing(self._p, ms, 8, calls, 1 if reset else 0))
+        out = {k: ms[i] for i, k in enumerate(self.HOST_PHASES)}
+        out.update({"prepares": calls[0], "fetches": calls[1], "host_threads": calls[2]})
+        return out
+
     def stats(self):
         st = BgStats()
         check(lib().bg_get_stats(self._p, ctypes.byref(st)))

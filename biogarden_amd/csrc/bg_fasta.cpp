@@ -12,7 +12,9 @@
 //     the next line beginning with '>';
 //   * read_all (:125-135) stops at the first empty record (no id, no desc, no residues), which is
 //     also what EOF returns.
-// Whitespace is Rust's char::is_whitespace (Unicode White_Space) on UTF-8 text.
+// Whitespace is Rust's char::is_whitespace (Unicode White_Space) on UTF-8 text.  Every line is
+// UTF-8 validated as BufRead::read_line does (:97, :115): an invalid line fails the read with
+// BG_E_UTF8 (io::ErrorKind::InvalidData, "stream did not contain valid UTF-8").
 //
 // Input is read in large blocks (BG_FASTA_BLOCK bytes, default 4 MiB) and split into lines with
 // memchr; a line spanning two blocks is carried over.
@@ -42,6 +44,38 @@ inline size_t ws_at(const uint8_t* p, const uint8_t* end) {
     if (c == 0xE3 && p[1] == 0x80 && p[2] == 0x80) return 3;                     // U+3000
   }
   return 0;
+}
+
+// str::from_utf8's rules (no overlong forms, no surrogates, nothing above U+10FFFF)
+inline bool utf8_valid(const uint8_t* p, size_t n) {
+  size_t i = 0;
+  while (i < n) {
+    // ASCII fast path, 8 bytes at a time
+    while (i + 8 <= n) {
+      uint64_t w;
+      std::memcpy(&w, p + i, 8);
+      if (w & 0x8080808080808080ull) break;
+      i += 8;
+    }
+    if (i >= n) break;
+    const uint8_t c = p[i];
+    if (c < 0x80) { ++i; continue; }
+    size_t len;
+    uint8_t lo = 0x80, hi = 0xBF;                      // bounds of the second byte
+    if (c >= 0xC2 && c <= 0xDF) len = 2;
+    else if (c == 0xE0) { len = 3; lo = 0xA0; }
+    else if (c == 0xED) { len = 3; hi = 0x9F; }
+    else if (c >= 0xE1 && c <= 0xEF) len = 3;
+    else if (c == 0xF0) { len = 4; lo = 0x90; }
+    else if (c == 0xF4) { len = 4; hi = 0x8F; }
+    else if (c >= 0xF1 && c <= 0xF3) len = 4;
+    else return false;
+    if (i + len > n || p[i + 1] < lo || p[i + 1] > hi) return false;
+    for (size_t k = 2; k < len; ++k)
+      if ((p[i + k] & 0xC0) != 0x80) return false;
+    i += len;
+  }
+  return true;
 }
 
 // str::trim_end: the length of [b, e) without its trailing whitespace characters
@@ -117,7 +151,8 @@ extern "C" void bg_fasta_close(bg_fasta* r) {
 
 extern "C" long bg_fasta_next_batch(bg_fasta* r, size_t max_records, size_t max_residues,
                                     bg_fasta_batch* out) {
-  if (!r || !out || max_records == 0) return BG_E_ARG;
+  // max_residues == 0 could never hold a record: refused rather than read as end of file
+  if (!r || !out || max_records == 0 || max_residues == 0) return BG_E_ARG;
   r->seq.clear();
   r->text.clear();
   r->seqOff.assign(1, 0);
@@ -133,6 +168,7 @@ extern "C" long bg_fasta_next_batch(bg_fasta* r, size_t max_records, size_t max_
       r->havePending = true;
     }
     const std::string& hl = r->pending;
+    if (!utf8_valid(reinterpret_cast<const uint8_t*>(hl.data()), hl.size())) return BG_E_UTF8;
     if (hl.empty() || hl[0] != '>') return BG_E_FORMAT;            // "Expected > at record start."
     const uint8_t* hb = reinterpret_cast<const uint8_t*>(hl.data()) + 1;
     const uint8_t* he = hb + trim_end_len(hb, reinterpret_cast<const uint8_t*>(hl.data()) + hl.size());
@@ -153,6 +189,8 @@ extern "C" long bg_fasta_next_batch(bg_fasta* r, size_t max_records, size_t max_
     r->havePending = false;
     for (;;) {
       if (!r->next_line(line)) break;
+      // read_line fails on the line it reads, the next record's header included (:115)
+      if (!utf8_valid(reinterpret_cast<const uint8_t*>(line.data()), line.size())) return BG_E_UTF8;
       if (line[0] == '>') { r->pending.swap(line); r->havePending = true; break; }
       const uint8_t* lb = reinterpret_cast<const uint8_t*>(line.data());
       r->seq.insert(r->seq.end(), lb, lb + trim_end_len(lb, lb + line.size()));

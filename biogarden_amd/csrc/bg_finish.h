@@ -783,8 +783,31 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                   bool busy = e2 != 0xFFFFFFFFu && (int)(e2 >> 4) == key;     // published meanwhile
                   for (int z = 0; z < nSlots; ++z) busy |= (sh[48 + z] != 0 && sh[40 + z] == key);
                   if (!busy) {
-                    // any slot not being filled: the walker reads nothing while it waits
-                    for (int z = 0; z < nSlots && zz < 0; ++z) if (!sh[48 + z]) zz = z;
+                    // the helpers' eviction order: an empty, stale or dead slot first (dead =
+                    // right of / below the walker, never read again), then one outside the
+                    // walker's 2 x 2 chunk footprint (the neighbourhood decode after the miss
+                    // reads those), then any slot not being filled
+                    const int vw = k > 0 ? k - 1 : 0;
+                    const int sw = vw / ROWS, remw = vw - sw * ROWS, ccw = (l + remw / R) >> 6;
+                    const int xA = (l + 63) >> 6;
+                    for (int pass = 0; pass < 3 && zz < 0; ++pass)
+                      for (int z = 0; z < nSlots && zz < 0; ++z) {
+                        if (sh[48 + z]) continue;
+                        const int oz = sh[40 + z];
+                        const int ss = oz >> 16, cc = oz & 0xffff;
+                        bool take;
+                        if (pass == 0) {
+                          const unsigned e = oz < 0 ? 0xFFFFFFFFu : ckMap[ck_map_idx(ss, cc)];
+                          take = oz < 0 || (e & 15) != (unsigned)z || (int)(e >> 4) != oz ||
+                                 ss > sw || (ss == sw && cc > ccw);
+                        } else if (pass == 1) {
+                          take = !((ss == sw && (cc == ccw || cc == ccw - 1)) ||
+                                   (ss == sw - 1 && (cc == xA || cc == xA - 1)));
+                        } else {
+                          take = true;
+                        }
+                        if (take) zz = z;
+                      }
                     if (zz >= 0) {
                       const int oz = sh[40 + zz];
                       if (oz >= 0) {

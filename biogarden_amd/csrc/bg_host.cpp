@@ -7,13 +7,17 @@
 //   score closure        score.rs:38-41 (+ A.8 tabulation: bg_scoring)
 //   buffer semantics     aligner.rs:92-94, 594-602 (exact-size here; divergences are flagged)
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <numeric>
 #include <thread>
 #include <vector>
@@ -91,25 +95,109 @@ struct PinBuf {
 
 inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
-// Host worker threads for the byte passes of prepare / fetch: at most 16 (a GPU's share of the
-// host's cores on the MI355X nodes), one per ~256 KiB of input, BG_HOST_THREADS overrides.
+// CPUs this process may run on: its affinity mask, bounded by the cgroup's CPU quota (threads
+// beyond the quota only time-share it, and a burst over it is throttled for the rest of the
+// scheduler period).  The MI355X boxes show 256 CPUs with a 16-CPU quota per GPU.
+int usable_cpus() {
+  static const int n = [] {
+    int c = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) c = CPU_COUNT(&set);
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long per = 0;
+      if (std::fscanf(f, "%31s %ld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0)
+        c = std::min(c, std::max(1, (int)(std::atol(q) / per)));
+      std::fclose(f);
+    }
+    return std::max(1, c);
+  }();
+  return n;
+}
+
+// Host threads for the byte passes of prepare / fetch: at most 16 (a GPU's share of the host's
+// cores on the MI355X nodes) and the usable CPUs, one per ~256 KiB of input; BG_HOST_THREADS
+// overrides.
 int host_threads(uint64_t bytes) {
-  int t = 16;
+  int t = std::min(16, usable_cpus());
   if (const char* e = std::getenv("BG_HOST_THREADS")) t = std::max(1, std::atoi(e));
-  const unsigned hw = std::thread::hardware_concurrency();
-  if (hw) t = std::min<int>(t, (int)hw);
   return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)t, bytes / (256 << 10) + 1));
 }
 
+// A persistent pool of host worker threads for the byte passes (created once, reused by every
+// handle): a parallel region costs two condition-variable hand-offs instead of a thread
+// creation and join per worker per call (16 of them per prepare and per fetch, ~1 ms a batch on
+// the streaming path).  One region at a time; the calling thread takes a share of the tasks.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool();   // never destroyed: workers may outlive static dtors
+    return *p;
+  }
+  // runs f(0) .. f(n - 1), at most one task per thread at a time, returns when all are done
+  template <class F>
+  void run(int n, const F& f) {
+    if (n <= 1) { if (n == 1) f(0); return; }
+    std::lock_guard<std::mutex> region(callM_);
+    const int want = n - 1;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      while ((int)th_.size() < want) th_.emplace_back([this] { worker(); });
+      task_ = [&f](int k) { f(k); };
+      ntasks_ = n;
+      next_ = 0;
+      finished_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [this] { return finished_ == ntasks_; });
+    task_ = nullptr;
+  }
+
+ private:
+  void drain() {
+    for (;;) {
+      int k;
+      {
+        std::lock_guard<std::mutex> g(m_);
+        if (next_ >= ntasks_) return;
+        k = next_++;
+      }
+      task_(k);
+      std::lock_guard<std::mutex> g(m_);
+      if (++finished_ == ntasks_) done_.notify_all();
+    }
+  }
+  void worker() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      drain();
+    }
+  }
+  std::mutex callM_, m_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  std::function<void(int)> task_;
+  int ntasks_ = 0, next_ = 0, finished_ = 0;
+  uint64_t gen_ = 0;
+};
+
 // Runs fn(lo, hi) over [0, n) split into contiguous ranges of about equal weight
-// (weight(i) = bytes of item i), one per thread; inline when one thread suffices.
+// (weight(i) = bytes of item i), one per pool task; inline when one thread suffices.
 template <class Wt, class F>
 void par_ranges(size_t n, Wt weight, F fn) {
   uint64_t total = 0;
   for (size_t i = 0; i < n; ++i) total += weight(i);
   const int T = host_threads(total);
   if (T <= 1 || n < 2) { fn((size_t)0, n); return; }
-  std::vector<std::thread> th;
+  std::vector<size_t> cut(1, 0);
   size_t lo = 0;
   uint64_t acc = 0;
   for (int k = 0; k < T && lo < n; ++k) {
@@ -117,10 +205,11 @@ void par_ranges(size_t n, Wt weight, F fn) {
     size_t hi = lo;
     while (hi < n && (acc < goal || hi == lo)) acc += weight(hi++);
     if (k == T - 1) hi = n;
-    th.emplace_back(fn, lo, hi);
+    cut.push_back(hi);
     lo = hi;
   }
-  for (auto& x : th) x.join();
+  if (cut.back() < n) cut.back() = n;
+  HostPool::get().run((int)cut.size() - 1, [&](int k) { fn(cut[k], cut[k + 1]); });
 }
 
 // The score closure tabulated over the codes a batch may use: code[byte] (0xFFFF:
@@ -134,20 +223,25 @@ struct HScore {
   int32_t at(int q, int c) const { return tab[(size_t)q * K + c]; }
 };
 
-// BG_PREPARE_TIMING: wall time of bg_batch_prepare's phases on stderr
+// Host-side phases of prepare / fetch, accumulated per handle (bg_host_timing) and, with
+// BG_PREPARE_TIMING set, printed per call on stderr
+enum { kPhSync, kPhStage, kPhPlan, kPhAlloc, kPhUpload, kPhFetchWait, kPhFetchCopy, kPhFetchUnpack, kPhN };
 struct PhaseTimer {
+  double* acc;
   bool on = std::getenv("BG_PREPARE_TIMING") != nullptr;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   char buf[512];
   int n = 0;
-  void mark(const char* what) {
-    if (!on) return;
+  explicit PhaseTimer(double* a) : acc(a) { buf[0] = 0; }
+  void mark(int ph, const char* what) {
     const auto now = std::chrono::steady_clock::now();
-    n += std::snprintf(buf + n, sizeof(buf) - n > 0 ? sizeof(buf) - n : 0, " %s %.3f", what,
-                       std::chrono::duration<double, std::milli>(now - t).count());
+    const double ms = std::chrono::duration<double, std::milli>(now - t).count();
     t = now;
+    acc[ph] += ms;
+    if (on)
+      n += std::snprintf(buf + n, sizeof(buf) - n > 0 ? sizeof(buf) - n : 0, " %s %.3f", what, ms);
   }
-  ~PhaseTimer() { if (on) std::fprintf(stderr, "prepare ms:%s\n", buf); }
+  ~PhaseTimer() { if (on && n) std::fprintf(stderr, "host ms:%s\n", buf); }
 };
 
 }  // namespace
@@ -230,7 +324,10 @@ struct bg_aligner {
   // bufAt[p] is the state pair p's call starts from (what bg_ref_divergent judges it against).
   long bufRows = 1024, bufCols = 1024;
   std::vector<std::pair<long, long>> bufAt;
+  std::vector<std::pair<long, long>> callDims;   // bg_aligner_set_call_dims: pending per-pair dims
   int finWaves = 0, finSlots = 0;   // last prepared batch: finish workgroup geometry
+  double hostMs[kPhN] = {0, 0, 0, 0, 0, 0, 0, 0};   // bg_host_timing: host phases, accumulated
+  uint64_t nPrepare = 0, nFetch = 0;
 
   size_t device_bytes() const {
     size_t t = seq1.cap + seq2.cap + codes1.cap + codes2.cap + lut.cap + prof.cap + pairs.cap + recs.cap;
@@ -274,6 +371,7 @@ extern "C" const char* bg_status_string(int s) {
     case BG_E_SCORE_RANGE: return "lengths beyond the LCS value frame";
     case BG_E_IO: return "cannot open file";
     case BG_E_FORMAT: return "Expected > at record start.";
+    case BG_E_UTF8: return "stream did not contain valid UTF-8";
     case BG_E_NO_BATCH: return "no prepared batch";
     case BG_E_ALPHABET: return "more than ~150 symbols with scores beyond int16";
     default: return "unknown";
@@ -663,12 +761,15 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
                         const HScore& S, int32_t a, int32_t b) {
   if (!h || mode < BG_GLOBAL || mode > BG_SEMIGLOBAL || S.K < 1 || S.K > 256) return BG_E_ARG;
   if (npairs && (!s1 || !n1 || !s2 || !n2)) return BG_E_ARG;
-  PhaseTimer tm;
+  std::vector<std::pair<long, long>> callDims;   // consumed by this prepare (aligner calls only)
+  if (!h->finFlags) callDims.swap(h->callDims);
+  PhaseTimer tm(h->hostMs);
+  ++h->nPrepare;
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
-  tm.mark("sync");
+  tm.mark(kPhSync, "sync");
   for (Slot& S : h->slot) S.inflight = false;
   h->execCount = 0;
   h->prepared = false;
@@ -771,13 +872,18 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
     }
   }
 
-  tm.mark("validate");
+  tm.mark(kPhStage, "validate+stage");
   // ---- the reference's scratch history over the batch's calls (aligner.rs:92-94): the
   // argument errors return before the resize, everything else (the score panic included)
   // resizes first.  Edit distance and LCS do not use a SequenceAligner.
+  // A shard's calls may start from dims given per pair (bg_aligner_set_call_dims): the history
+  // of the whole batch, replayed by the caller; the dims after the shard follow its last call.
+  const bool given = !callDims.empty();
+  if (given && callDims.size() != npairs) return BG_E_ARG;
   long bufR = h->bufRows, bufC = h->bufCols;
   h->bufAt.assign(npairs, std::make_pair(bufR, bufC));
   for (size_t p = 0; p < npairs; ++p) {
+    if (given) { bufR = callDims[p].first; bufC = callDims[p].second; }
     h->bufAt[p] = std::make_pair(bufR, bufC);
     if (h->finFlags || h->prestatus[p] == BG_INVALID_ARGUMENT_RANGE ||
         h->prestatus[p] == BG_INVALID_INPUT_SIZE)
@@ -862,7 +968,7 @@ plan_again:
     ckLimit = true;
     goto plan_again;
   }
-  tm.mark("plan");
+  tm.mark(kPhPlan, "plan");
   size_t lds = 0;
   if (h->tag) {
     // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
@@ -984,7 +1090,7 @@ plan_again:
   h->bndBytes = bo * 4 * ((h->affine || h->ack) ? 2 : 1);
   h->resBytes = o1 + o2;
 
-  tm.mark("layout");
+  tm.mark(kPhPlan, "layout");
   // ---- device memory
   if (!h->seq1.ensure(o1 + 16) || !h->seq2.ensure(o2 + 16) || !h->codes1.ensure(o1 + 16) ||
       !h->codes2.ensure(o2 + 16) || !h->lut.ensure(256) ||
@@ -1002,7 +1108,7 @@ plan_again:
       return BG_E_NOMEM;
   }
 
-  tm.mark("alloc");
+  tm.mark(kPhAlloc, "alloc");
   // ---- uploads: the raw residues staged above (one DMA each), the tables; the codes are
   // made on the device (bg_code_kernel)
   uint8_t lut[256];
@@ -1093,14 +1199,14 @@ plan_again:
       BG_HIP(hipMemcpyAsync(h->recs.p, tmpl.data(), sizeof(BgPairResultDev) * npairs,
                             hipMemcpyHostToDevice, h->stream));
   }
-  tm.mark("queue");
+  tm.mark(kPhUpload, "queue");
   BG_HIP(hipStreamSynchronize(h->stream));
-  tm.mark("upload");
+  tm.mark(kPhUpload, "upload");
   h->order_ = order;
   h->bufRows = bufR;
   h->bufCols = bufC;
   fin_geom(h, h->plan.size(), &h->finWaves, &h->finSlots);
-  tm.mark("fin_geom");
+  tm.mark(kPhPlan, "fin_geom");
   h->prepared = true;
   return BG_OK;
 }
@@ -1290,8 +1396,11 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   if (!h || (h->npairs && !res)) return BG_E_ARG;
   if (!h->prepared || !h->executed) return BG_E_NO_BATCH;
   if (h->outBytes && (!out1 || !out2 || out_cap < h->outBytes)) return BG_E_ARG;
+  PhaseTimer tm(h->hostMs);
+  ++h->nFetch;
   int rc = bg_synchronize(h);
   if (rc) return rc;
+  tm.mark(kPhFetchWait, "fetch-wait");
   const size_t np = h->plan.size();
   if (std::getenv("BG_DP_TIMING") && h->dpDbg.p && np) {
     // first pair's waves: strip start / chunk-0 end / strip end relative to the earliest start
@@ -1333,6 +1442,7 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
     BG_HIP(hipMemcpyAsync(h->ho2.p, S.out2.p, ob, hipMemcpyDeviceToHost, h->stream));
     BG_HIP(hipStreamSynchronize(h->stream));
   }
+  tm.mark(kPhFetchCopy, "fetch-d2h");
   for (size_t p = 0; p < h->npairs; ++p) {
     std::memset(&res[p], 0, sizeof(res[p]));
     res[p].status = h->prestatus[p] < 0 ? 0 : h->prestatus[p];
@@ -1366,7 +1476,19 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
         o.status = BG_REF_DIVERGENT;
     }
   });
+  tm.mark(kPhFetchUnpack, "fetch-unpack");
   return BG_OK;
+}
+
+extern "C" int bg_host_timing(bg_aligner* h, double* ms, size_t n, uint64_t* calls, int reset) {
+  if (!h || (n && !ms)) return BG_E_ARG;
+  for (size_t i = 0; i < n && i < (size_t)kPhN; ++i) ms[i] = h->hostMs[i];
+  if (calls) { calls[0] = h->nPrepare; calls[1] = h->nFetch; calls[2] = (uint64_t)host_threads(~0ull); }
+  if (reset) {
+    for (double& x : h->hostMs) x = 0.0;
+    h->nPrepare = h->nFetch = 0;
+  }
+  return kPhN;
 }
 
 extern "C" int bg_align_batch(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
@@ -1423,6 +1545,18 @@ extern "C" int bg_aligner_set_buffer_size(bg_aligner* h, size_t rows, size_t col
   if (!h || rows > 0x7FFFFFFF || cols > 0x7FFFFFFF) return BG_E_ARG;
   h->bufRows = (long)rows;
   h->bufCols = (long)cols;
+  return BG_OK;
+}
+
+extern "C" int bg_aligner_set_call_dims(bg_aligner* h, size_t npairs, const uint64_t* rows,
+                                        const uint64_t* cols) {
+  if (!h) return BG_E_ARG;
+  h->callDims.clear();
+  if (!npairs || !rows || !cols) return BG_OK;
+  for (size_t p = 0; p < npairs; ++p)
+    if (rows[p] > 0x7FFFFFFF || cols[p] > 0x7FFFFFFF) return BG_E_ARG;
+  h->callDims.resize(npairs);
+  for (size_t p = 0; p < npairs; ++p) h->callDims[p] = std::make_pair((long)rows[p], (long)cols[p]);
   return BG_OK;
 }
 

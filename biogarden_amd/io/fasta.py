@@ -59,6 +59,10 @@ _WS = frozenset("\t\n\x0b\x0c\r \x85\xa0\u1680\u2000\u2001\u2002\u2003\u2004\u20
                 "\u2006\u2007\u2008\u2009\u200a\u2028\u2029\u202f\u205f\u3000")
 
 
+# std's message for BufRead::read_line on bytes that are not UTF-8 (io::ErrorKind::InvalidData)
+UTF8_ERROR = "stream did not contain valid UTF-8"
+
+
 def _trim_end(s):
     return s.rstrip("".join(_WS))
 
@@ -75,10 +79,16 @@ class Reader:
         except OSError as e:
             raise IOError("Failed to read fasta from %r" % (str(path),)) from e
 
+    def _readline(self):
+        try:
+            return self._r.readline()
+        except UnicodeDecodeError as e:
+            raise IOError(UTF8_ERROR) from e
+
     def read(self, record):
         record.clear()
         if not self._line:
-            self._line = self._r.readline()
+            self._line = self._readline()
             if not self._line:
                 return
         if not self._line.startswith(">"):
@@ -91,7 +101,7 @@ class Reader:
         else:
             record._id, record._desc = head[:cut], head[cut + 1:]
         while True:
-            self._line = self._r.readline()
+            self._line = self._readline()
             if not self._line or self._line.startswith(">"):
                 break
             record._seq.extend(_trim_end(self._line).encode())
@@ -180,6 +190,8 @@ class BatchReader:
     def __init__(self, path, max_records=65536, max_residues=64 << 20):
         import ctypes
         from .. import _native
+        if max_records < 1 or max_residues < 1:
+            raise ValueError("max_records and max_residues must be positive")
         self._n = _native
         err = ctypes.c_int(0)
         self._r = _native.lib().bg_fasta_open(str(path).encode(), ctypes.byref(err))
@@ -197,6 +209,8 @@ class BatchReader:
         if rc < 0:
             if rc == -8:
                 raise IOError("Expected > at record start.")
+            if rc == -9:
+                raise IOError(UTF8_ERROR)
             self._n.check(rc)
         n = b.n
         if n == 0:

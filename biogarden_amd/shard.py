@@ -4,12 +4,44 @@ One process per GPU.  A batch is split over ranks by cells (largest-first greedy
 in-GPU pair plan); every rank runs its shard through its own `bg_aligner`, packs the results
 on the device with `bg_batch_export`, and rank 0 collects the packed records with one
 variable-size gather (RCCL over xGMI with backend "nccl", gloo on CPU).  No collective is on
-the data path: the pairs share nothing (reference: one `SequenceAligner` call per pair,
-src/alignment/aligner.rs:84-435).
+the data path: the pairs' answers share nothing (reference: one `SequenceAligner` call per
+pair, src/alignment/aligner.rs:84-435).
+
+The one thing the reference carries from call to call is its aligner's scratch dims
+(aligner.rs:92-94, 594-602), which decide the reference-divergence flag (status 4).  Every rank
+replays that history over the WHOLE batch in caller order (`call_dims`, a host prefix scan) and
+hands its shard the dims each of its pairs starts from (`Handle.set_call_dims`), so the merged
+statuses equal one aligner's run of the batch exactly.
 """
 import struct
 
 from . import _native
+
+_NONPOS = ("global", "local", "fitting")
+
+
+def call_dims(mode, sizes, a, b, start=(1024, 1024)):
+    """Scratch dims each call of a batch starts from, in caller order: one reference
+    SequenceAligner (1024 x 1024 when new, aligner.rs:44-55) running every pair.  A call resizes
+    to (n1 + 1, n2 + 1) when n1 > rows or n2 > cols (:92-94, 594-602); the argument errors
+    (InvalidArgumentRange :87-89 / 153-155 / 219-221, fitting's InvalidInputSize :223-225) return
+    before that.  sizes: list of (n1, n2).  Returns a list of (rows, cols)."""
+    rows, cols = start
+    out = []
+    bad_args = mode in _NONPOS and (a > 0 or b > 0)
+    for n1, n2 in sizes:
+        out.append((rows, cols))
+        if bad_args or (mode == "fitting" and n1 < n2):
+            continue
+        if n1 > rows or n2 > cols:
+            rows, cols = n1 + 1, n2 + 1
+    return out
+
+
+def shard_call_dims(mode, sizes, a, b, shard_idx, start=(1024, 1024)):
+    """call_dims of the whole batch, restricted to one shard's pairs (in the shard's order)."""
+    d = call_dims(mode, sizes, a, b, start)
+    return [d[p] for p in shard_idx]
 
 
 def lpt_shards(sizes, world):

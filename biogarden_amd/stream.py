@@ -43,6 +43,9 @@ class AlignStream:
             h.set_pipeline(pipeline)
         self._next = 0
         self._inflight = deque()            # (handle index, tag, panics, pairs-or-None)
+        # batches collected to free a handle whose submit then failed (prepare / execute raised):
+        # handed out first by the next submit or drain, so no result is lost
+        self._pending = []
         # the stream is ONE reference aligner: its scratch dims (aligner.rs:92-94, which decide
         # the reference-divergence flag, status 4) pass from handle to handle in call order
         self._buf = self._hs[0].buffer_size()
@@ -68,8 +71,9 @@ class AlignStream:
         return tag, res
 
     def _slot(self):
-        """The next handle of the rotation, after collecting the batch it still holds."""
-        ready = []
+        """The next handle of the rotation, after collecting the batch it still holds (plus any
+        batches a failed submit collected earlier)."""
+        ready, self._pending = self._pending, []
         hi = self._next
         if any(x[0] == hi for x in self._inflight):
             while self._inflight and self._inflight[0][0] != hi:
@@ -85,10 +89,14 @@ class AlignStream:
         sc, panics = _score.tabulate(self.score, pairs)
         hi, ready = self._slot()
         h = self._hs[hi]
-        h.set_buffer_size(*self._buf)
-        h.prepare(self.mode, pairs, sc, self.a, self.b)
-        self._buf = h.buffer_size()
-        h.execute()
+        try:
+            h.set_buffer_size(*self._buf)
+            h.prepare(self.mode, pairs, sc, self.a, self.b)
+            self._buf = h.buffer_size()
+            h.execute()
+        except Exception:
+            self._pending = ready           # returned by the next submit / drain
+            raise
         self._inflight.append((hi, tag, panics, pairs if panics else None))
         return ready
 
@@ -98,10 +106,14 @@ class AlignStream:
         sc, panics = _score.tabulate(self.score, [(buf1, buf2)])
         hi, ready = self._slot()
         h = self._hs[hi]
-        h.set_buffer_size(*self._buf)
-        h.prepare_packed(self.mode, buf1, off1, idx1, buf2, off2, idx2, sc, self.a, self.b)
-        self._buf = h.buffer_size()
-        h.execute()
+        try:
+            h.set_buffer_size(*self._buf)
+            h.prepare_packed(self.mode, buf1, off1, idx1, buf2, off2, idx2, sc, self.a, self.b)
+            self._buf = h.buffer_size()
+            h.execute()
+        except Exception:
+            self._pending = ready
+            raise
         keys = None
         if panics:
             keys = [(buf1[off1[i]:off1[i + 1]], buf2[off2[j]:off2[j + 1]]) for i, j in zip(idx1, idx2)]
@@ -110,16 +122,26 @@ class AlignStream:
 
     def drain(self):
         """Collects every batch still in flight: a list of (tag, results), oldest first."""
-        out = []
+        out, self._pending = self._pending, []
         while self._inflight:
             out.append(self._collect())
         return out
+
+    def host_timing(self, reset=False):
+        """Host-side ms per prepare / fetch phase summed over the rotation's handles
+        (Handle.host_timing)."""
+        tot = {}
+        for h in self._hs:
+            for k, v in h.host_timing(reset).items():
+                tot[k] = max(tot.get(k, 0), v) if k == "host_threads" else tot.get(k, 0) + v
+        return tot
 
     def close(self):
         for h in self._hs:
             h.close()
         self._hs = []
         self._inflight.clear()
+        self._pending = []
 
 
 def align_stream(mode, batches, score, a, b, **kw):

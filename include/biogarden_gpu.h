@@ -62,7 +62,9 @@ enum {
   BG_E_NO_BATCH = -5,   /* bg_batch_execute/fetch without a prepared batch */
   BG_E_ALPHABET = -6,   /* more than ~150 symbols in a batch whose scores leave int16 */
   BG_E_IO = -7,         /* bg_fasta_open: the file cannot be opened */
-  BG_E_FORMAT = -8      /* bg_fasta_next_batch: "Expected > at record start." (fasta.rs:104-109) */
+  BG_E_FORMAT = -8,     /* bg_fasta_next_batch: "Expected > at record start." (fasta.rs:104-109) */
+  BG_E_UTF8 = -9        /* bg_fasta_next_batch: a line is not valid UTF-8 (BufRead::read_line's
+                           io::ErrorKind::InvalidData, fasta.rs:97, 115) */
 };
 
 /* Scoring closure as data: code[byte] in [0, alphabet_size) or 0xFF when the closure would
@@ -170,12 +172,30 @@ int bg_aligner_buffer_size(bg_aligner* h, size_t* rows, size_t* cols);
  * stand for ONE reference aligner — the streaming rotation of biogarden_amd/stream.py — pass
  * the state on in call order. */
 int bg_aligner_set_buffer_size(bg_aligner* h, size_t rows, size_t cols);
+/* The dims each call of the NEXT prepared batch starts from, given per pair: a shard of a larger
+ * batch whose earlier calls ran on other ranks (biogarden_amd/shard.py call_dims replays the
+ * resize rule over the whole batch in caller order, so every rank judges status BG_REF_DIVERGENT
+ * against the history one reference aligner fed the whole batch would have).  rows / cols hold
+ * npairs entries; the next bg_batch_prepare / bg_batch_prepare_table must have exactly npairs
+ * pairs (else it returns BG_E_ARG) and consumes them; afterwards the handle's dims are what the
+ * last pair's call leaves.  npairs = 0 or NULL arrays clear a pending set. */
+int bg_aligner_set_call_dims(bg_aligner* h, size_t npairs, const uint64_t* rows, const uint64_t* cols);
 
 /* Kernel timing over a region of executes (HIP events recorded on the handle's stream around
  * the DP and the finish kernel of every execute; up to 4096 executes per region).
  * bg_profile_end waits for the work and returns per-execute averages in milliseconds. */
 int bg_profile_begin(bg_aligner* h);
 int bg_profile_end(bg_aligner* h, float* avg_dp_ms, float* avg_finish_ms, int* executes);
+
+/* Host-side time of this handle's bg_batch_prepare / bg_batch_fetch calls, accumulated (ms):
+ *   ms[0] waiting for the handle's previous work   ms[1] validation + staging (byte pass)
+ *   ms[2] planning (history, alphabet, geometry)   ms[3] device allocation
+ *   ms[4] upload (queue + wait)                    ms[5] fetch: waiting for the kernels
+ *   ms[6] fetch: device-to-host copies             ms[7] fetch: string unpacking (byte pass)
+ * Up to n entries are written; calls (3 entries, may be NULL) receives the prepare count, the
+ * fetch count and the host threads the byte passes use.  reset != 0 zeroes the totals after
+ * reading.  Returns the number of phases (8). */
+int bg_host_timing(bg_aligner* h, double* ms, size_t n, uint64_t* calls, int reset);
 
 /* Device-to-device export of the last execute's results for a collective (e.g. an RCCL
  * gather to rank 0): dst (device memory, same GPU) receives the packed record
@@ -233,7 +253,8 @@ typedef struct bg_fasta_batch {
 } bg_fasta_batch;
 bg_fasta* bg_fasta_open(const char* path, int* err);        /* err: 0, BG_E_ARG or BG_E_IO */
 long bg_fasta_next_batch(bg_fasta* r, size_t max_records, size_t max_residues,
-                         bg_fasta_batch* out);               /* records, or BG_E_* (< 0) */
+                         bg_fasta_batch* out);               /* records, or BG_E_* (< 0); both
+                                                                maxima must be > 0 (BG_E_ARG) */
 void bg_fasta_close(bg_fasta* r);
 
 const char* bg_status_string(int status);

@@ -37,8 +37,20 @@ def check_batch(aligner, oracle, mode, pairs, scoring, a, b, fresh=True, sample=
     dims = aligner.buffer_size
     res = aligner.align_batch(mode, pairs, getattr(score_mod, scoring) if isinstance(scoring, str)
                               else scoring, a, b)
+    ref = check_results(oracle, mode, pairs, res, scoring, a, b,
+                        dims=dims if (fresh and sample is None) else None, sample=sample)
+    if ref is not None:
+        assert aligner.buffer_size == ref.buffer_size(), (aligner.buffer_size, ref.buffer_size())
+    return res
+
+
+def check_results(oracle, mode, pairs, res, scoring, a, b, dims=None, sample=None, ref=None):
+    """check_batch's comparison for results produced elsewhere (a stream, a merged shard): `res`
+    are AlignmentResults in pair order.  `dims`: replay a reference-faithful aligner from these
+    scratch dims over every pair (or pass a running one as `ref`); returns that aligner."""
     sc_or = scoring if isinstance(scoring, str) else oracle.scoring(scoring)
-    ref = oracle.Aligner(dims=dims) if (fresh and sample is None) else None
+    if ref is None and dims is not None:
+        ref = oracle.Aligner(dims=dims)
     idx = range(len(pairs)) if sample is None else sample
     bad = []
     for p in idx:
@@ -65,10 +77,8 @@ def check_batch(aligner, oracle, mode, pairs, scoring, a, b, fresh=True, sample=
                     bad.append(("ref-ok", p, len(s1), len(s2), fst, r.status, fsc, r[0]))
             elif r.status == 0:
                 bad.append(("ref-panics-but-ok", p, len(s1), len(s2), fst, s1[:30], s2[:30]))
-    if ref is not None:
-        assert aligner.buffer_size == ref.buffer_size(), (aligner.buffer_size, ref.buffer_size())
     assert not bad, bad[:5]
-    return res
+    return ref
 
 
 def sample_indices(n, k, seed):

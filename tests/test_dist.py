@@ -161,3 +161,28 @@ def test_gather_two_ranks_gloo():
     assert msg[0] == "ok", msg
     assert msg[1] and msg[2] == 23 and msg[3]
     assert all(p.exitcode == 0 for p in procs)
+
+
+@pytest.mark.parametrize("mode,a,b", [("global", -11, -1), ("local", -11, -1), ("fitting", -1, -1),
+                                      ("overlap", -2, -2), ("semiglobal", -1, -2),
+                                      ("global", 1, -1)])
+def test_call_dims_follow_the_reference_aligner(mode, a, b):
+    """shard.call_dims (the per-pair scratch dims every rank replays over the whole batch) equals
+    the dims a reference-faithful SequenceAligner (oracle/refcpu.c, aligner.rs:44-55, 92-94,
+    594-602) holds before each call, through argument errors, fitting's size error, equal-size
+    and larger pairs."""
+    from oracle import refcpu
+    rng = random.Random(hash((mode, a, b)) & 0xFFFF)
+    lens = [0, 1, 2, 7, 40, 1023, 1024, 1025, 1100]
+    pairs = [(bytes(rng.choice(b"ACGT") for _ in range(rng.choice(lens))),
+              bytes(rng.choice(b"ACGT") for _ in range(rng.choice(lens)))) for _ in range(24)]
+    al = refcpu.Aligner(exact=False)
+    want = []
+    for s1, s2 in pairs:
+        want.append(al.buffer_size())
+        al.align(mode, s1, s2, "blosum62", a, b)
+    got = shard.call_dims(mode, [(len(x), len(y)) for x, y in pairs], a, b)
+    assert got == want
+    idx = [3, 0, 17, 9]
+    assert shard.shard_call_dims(mode, [(len(x), len(y)) for x, y in pairs], a, b, idx) == \
+        [want[p] for p in idx]

@@ -111,3 +111,56 @@ def test_empty_file(tmp_path):
     path = tmp_path / "z.fa"
     path.write_bytes(b"")
     assert _native_records(str(path), 10, 100) == ([], [])
+
+
+@pytest.mark.parametrize("data", [
+    b">a\nAC\xffGT\n>b\nGG\n",              # a byte that never starts UTF-8
+    b">a\xc3\n",                            # truncated two-byte form
+    b">a\nACGT\n>b \xed\xa0\x80\nGG\n",     # a surrogate (U+D800) in the next header
+    b">a\nAC\xc0\xafG\n",                   # overlong '/'
+    b">a\nAC\xf4\x90\x80\x80\n",            # above U+10FFFF
+])
+def test_invalid_utf8_is_an_error(tmp_path, data):
+    """BufRead::read_line fails on a line that is not UTF-8 (fasta.rs:97, 115): read_all returns
+    Err(InvalidData).  Both readers raise, at every block size."""
+    from biogarden_amd.io import fasta
+    path = tmp_path / "u.fa"
+    path.write_bytes(data)
+    with pytest.raises(IOError, match=fasta.UTF8_ERROR):
+        _py_records(str(path))
+    for block in (1, 3, None):
+        with pytest.raises(IOError, match=fasta.UTF8_ERROR):
+            _native_records(str(path), 10, 100, block)
+
+
+def test_valid_multibyte_utf8_is_accepted(tmp_path):
+    path = tmp_path / "m.fa"
+    path.write_bytes(">α β　desc\nAC\n>\U0001F600\nGT \n".encode("utf-8"))
+    want = _py_records(str(path))
+    assert want == [("α", "β　desc", b"AC"), ("\U0001F600", None, b"GT")]
+    assert _native_records(str(path), 10, 100, 2)[0] == want
+
+
+@pytest.mark.parametrize("maxr,maxres", [(0, 100), (10, 0)])
+def test_zero_batch_limits_are_refused(tmp_path, maxr, maxres):
+    from biogarden_amd.io import fasta
+    path = tmp_path / "z.fa"
+    path.write_bytes(b">a\nAC\n")
+    with pytest.raises(ValueError):
+        fasta.BatchReader(str(path), max_records=maxr, max_residues=maxres)
+
+
+def test_zero_max_residues_is_refused_by_the_abi(tmp_path):
+    import ctypes
+    from biogarden_amd import _native
+    path = tmp_path / "z.fa"
+    path.write_bytes(b">a\nAC\n")
+    L = _native.lib()
+    err = ctypes.c_int(0)
+    r = L.bg_fasta_open(str(path).encode(), ctypes.byref(err))
+    try:
+        b = _native.BgFastaBatch()
+        assert L.bg_fasta_next_batch(r, 10, 0, ctypes.byref(b)) == -1
+        assert L.bg_fasta_next_batch(r, 10, 100, ctypes.byref(b)) == 1
+    finally:
+        L.bg_fasta_close(r)

@@ -237,12 +237,16 @@ def test_beyond_checkpoint_chunk_keys(aligner, oracle, mode, a, b, n1, n2):
 def test_traceback_walker_self_service(aligner, oracle, slots):
     """BG_FIN_SELFSERVE: the walker recomputes every missed chunk itself instead of waiting for
     a helper (the path that guarantees forward progress when every helper is busy); with the
-    fewest slots the asynchronous form allows.  Same strings as the oracle."""
+    fewest slots the asynchronous form allows.  Same strings as the oracle, every status 0 (a
+    walker evicting a chunk it needs next would thrash into BG_INTERNAL)."""
     from biogarden_amd.alignment import score
     rng = random.Random(0x5E1F)
     base = rand_seq(rng, 6000, DNA)
+    # the last two walk (near-)diagonally from (6000, 6000): across every strip boundary at a
+    # chunk corner, where the walker's 2 x 2 chunk footprint matters for its own evictions
     pairs = [(base, base[:3000] + rand_seq(rng, 3000, DNA) + base[3000:]),
-             (base, base[:1500] + base[4000:]), (base, mutate(rng, base, DNA, 0.15))]
+             (base, base[:1500] + base[4000:]), (base, mutate(rng, base, DNA, 0.15)),
+             (base, base), (base, mutate(rng, base, DNA, 0.01))]
     expect = [oracle.align("semiglobal", s1, s2, "blosum62", -1, -2, exact=True) for s1, s2 in pairs]
     os.environ["BG_FIN_SELFSERVE"] = "1"
     os.environ["BG_FIN_SLOTS"] = slots

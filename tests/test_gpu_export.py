@@ -91,16 +91,25 @@ def test_lpt_sharded_handles_merge_to_single_run(world):
     from biogarden_amd import _native, shard
     sc = _native.builtin_scoring(_native.BG_BLOSUM62)
     pairs = _pairs(17 + world)
+    # an empty seq1 against a long seq2 resizes the reference's scratch to 1 x 3501 (flagged
+    # itself, aligner.rs:98-104); the calls after it then run on one row until a longer seq1
+    # resizes again (flagged when len1 == 1): the statuses depend on the whole batch's history
+    pairs[5:5] = [(b"", bytes(random.Random(3).choice(b"ACGT") for _ in range(3500)))]
+    pairs[6:6] = [(b"A", b"ACGT"), (b"C", b"CCGTA")]
     h = _native.Handle(0)
     try:
         single = h.align_batch("global", pairs, sc, -11, -1)
     finally:
         h.close()
-    shards = shard.lpt_shards([(len(x), len(y)) for x, y in pairs], world)
+    sizes = [(len(x), len(y)) for x, y in pairs]
+    shards = shard.lpt_shards(sizes, world)
     per = []
     for idx in shards:
         hr = _native.Handle(0)
         try:
+            # status 4 is judged against the scratch dims one reference aligner running the whole
+            # batch would hold before each call (aligner.rs:92-94): every rank replays that history
+            hr.set_call_dims(shard.shard_call_dims("global", sizes, -11, -1, idx))
             hr.prepare("global", [pairs[p] for p in idx], sc, -11, -1)
             hr.execute()
             hr.synchronize()
@@ -108,9 +117,18 @@ def test_lpt_sharded_handles_merge_to_single_run(world):
         finally:
             hr.close()
     merged = shard.merge_shards(shards, per)
-    # status 4 flags a pair the reference's reused aligner would answer differently (its scratch
-    # dims depend on the calls before it, aligner.rs:92-94); a shard replays a different call
-    # history than the single run, so 0 / 4 may differ — the answers themselves may not
-    strip = lambda r: (r["status"] if r["status"] not in (0, 4) else 0, r["score"],  # noqa: E731
-                       r["aligned1"], r["aligned2"], r["end"], r["start"])
-    assert [strip(r) for r in merged] == [strip(r) for r in single]
+    assert [r["status"] for r in single].count(4) > 0      # the flag is exercised
+    assert merged == single
+
+
+def test_call_dims_mismatch_is_rejected():
+    from biogarden_amd import _native
+    h = _native.Handle(0)
+    try:
+        h.set_call_dims([(1024, 1024)] * 3)
+        with pytest.raises(RuntimeError):
+            h.prepare("global", _pairs(1, n=2), _native.builtin_scoring(_native.BG_BLOSUM62), -11, -1)
+        # consumed: the next prepare runs from the handle's own history
+        h.prepare("global", _pairs(1, n=2), _native.builtin_scoring(_native.BG_BLOSUM62), -11, -1)
+    finally:
+        h.close()

@@ -1,12 +1,14 @@
 """Streaming ingest on the GPU (biogarden_amd.stream): reads and refs
 written as FASTA, read back in batches by the native BatchReader, queued through AlignStream's
 handle rotation straight from the packed batch buffers — every result (status, score, both
-aligned strings) equals one SequenceAligner.align_batch over the same pairs, in submission order."""
+aligned strings) is compared with the CPU oracle: the exact-size answer, and the status a
+reference-faithful aligner fed the same pairs in submission order would earn (the stream stands
+for ONE SequenceAligner, aligner.rs:92-94)."""
 import random
 
 import pytest
 
-from parity_util import DNA, mutate, rand_seq
+from parity_util import DNA, check_results, mutate, rand_seq
 
 pytestmark = pytest.mark.gpu
 
@@ -20,7 +22,7 @@ def _write_fasta(path, recs):
 
 
 @pytest.mark.parametrize("handles", [1, 2, 4])
-def test_fasta_reads_vs_refs_streamed(tmp_path, handles):
+def test_fasta_reads_vs_refs_streamed(tmp_path, handles, oracle):
     from biogarden_amd.alignment import score
     from biogarden_amd.alignment.aligner import SequenceAligner
     from biogarden_amd.io import fasta
@@ -47,20 +49,20 @@ def test_fasta_reads_vs_refs_streamed(tmp_path, handles):
         got += st.drain()
     assert [t for t, _ in got] == sorted(t for t, _ in got)
     flat = [r for _, rs in got for r in rs]
+    assert len(flat) == 300
+    pairs = [(reads[i], refs[which[i]]) for i in range(len(reads))]
+    check_results(oracle, "semiglobal", pairs, flat, "blosum62", -1, -2, dims=(1024, 1024))
+    # and the same as one aligner's batch (end cells included)
     al = SequenceAligner(0)
     try:
-        want = al.align_batch("semiglobal", [(reads[i], refs[which[i]]) for i in range(len(reads))],
-                              score.blosum62, -1, -2)
+        want = al.align_batch("semiglobal", pairs, score.blosum62, -1, -2)
     finally:
         al.close()
-    key = lambda r: (r.status, r[0], bytes(r[1].chain), bytes(r[2].chain), r.end)  # noqa: E731
-    assert len(flat) == len(want) == 300
-    assert [key(r) for r in flat] == [key(r) for r in want]
+    assert [r.end for r in flat] == [r.end for r in want]
 
 
-def test_align_stream_generator_mixed_batches():
+def test_align_stream_generator_mixed_batches(oracle):
     from biogarden_amd.alignment import score
-    from biogarden_amd.alignment.aligner import SequenceAligner
     from biogarden_amd.stream import align_stream
     rng = random.Random(7)
     batches = []
@@ -72,11 +74,29 @@ def test_align_stream_generator_mixed_batches():
         batches.append((t, pairs))
     out = list(align_stream("global", batches, score.blosum62, -11, -1, handles=3))
     assert [t for t, _ in out] == list(range(7))
-    al = SequenceAligner(0)
-    try:
-        for (t, pairs), (_, res) in zip(batches, out):
-            want = al.align_batch("global", pairs, score.blosum62, -11, -1) if pairs else []
-            assert [(r[0], bytes(r[1].chain), bytes(r[2].chain)) for r in res] == \
-                   [(r[0], bytes(r[1].chain), bytes(r[2].chain)) for r in want]
-    finally:
-        al.close()
+    ref = oracle.Aligner(dims=(1024, 1024))      # one reference aligner across every batch
+    for (t, pairs), (_, res) in zip(batches, out):
+        assert len(res) == len(pairs)
+        check_results(oracle, "global", pairs, res, "blosum62", -11, -1, ref=ref)
+
+
+def test_failed_submit_keeps_collected_results(oracle):
+    """A submit that has to collect a finished batch to free its handle and then fails in
+    prepare hands the collected batch out with the next submit / drain: nothing is lost."""
+    from biogarden_amd.alignment import score
+    from biogarden_amd.stream import AlignStream
+    rng = random.Random(11)
+    batches = [[(rand_seq(rng, 200, DNA), rand_seq(rng, 180, DNA)) for _ in range(5)] for _ in range(4)]
+    seen = []
+    with AlignStream("global", score.blosum62, -11, -1, handles=2) as st:
+        seen += st.submit(batches[0], tag=0)
+        seen += st.submit(batches[1], tag=1)            # the rotation is full
+        st.mode = 99                                    # an unknown mode: prepare fails (BG_E_ARG)
+        with pytest.raises(RuntimeError):
+            st.submit(batches[2], tag=2)                # collected batch 0 first
+        st.mode = "global"
+        seen += st.submit(batches[3], tag=3)
+        seen += st.drain()
+    assert [t for t, _ in seen] == [0, 1, 3]
+    for t, res in seen:
+        check_results(oracle, "global", batches[t], res, "blosum62", -11, -1)

@@ -71,6 +71,13 @@ def main():
     for i, name in enumerate(args.configs):
         rng = np.random.default_rng(0xB10A11F0 + int(name[1:]))
         mode, pairs, a, b = config(name, rng, args.rank, args.world)
+        if name in ("C4", "C5"):      # the whole job's call history (status 4, shard.call_dims)
+            from biogarden_amd import shard
+            from tools import workloads
+            allp = workloads.job(name)[1]
+            sizes = [(len(x), len(y)) for x, y in allp]
+            idx = shard.lpt_shards(sizes, args.world)[args.rank]
+            h.set_call_dims(shard.shard_call_dims(mode, sizes, a, b, idx))
         t0 = time.perf_counter()
         h.prepare(mode, pairs, sc, a, b)
         prep = time.perf_counter() - t0

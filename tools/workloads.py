@@ -83,3 +83,27 @@ def metric_pairs(npairs=256, n1=10000, n2=10000, seed=None):
 
 def cells(pairs):
     return sum(len(x) * len(y) for x, y in pairs)
+
+
+# what each configuration is, for records
+DESCRIPTION = {
+    "C2": "1024 x (1000 x 1000) uniform DNA, local (Smith-Waterman) affine -11/-1, blosum62",
+    "C3": "1 x (100 000 x 100 000) uniform DNA, semiglobal -1/-2, blosum62 (intra-pair tiling)",
+    "C4": "65 536 reads (150 bp, 2 % substitutions) vs 64 refs of 10 kbp, semiglobal -1/-2, "
+          "blosum62 (seq1 = read)",
+    "C5": "all-vs-all of 256 proteins U[64, 4000] (32 640 pairs), global -11/-1, blosum62",
+}
+
+
+def job(name):
+    """A whole configuration as one batch: (mode, pairs, open, extend)."""
+    mode, _, a, b = PARAMS[name]
+    if name == "C2":
+        return mode, c2_pairs(), a, b
+    if name == "C3":
+        return mode, c3_pair(), a, b
+    if name == "C4":
+        return mode, c4_pairs(), a, b
+    if name == "C5":
+        return mode, c5_pairs(), a, b
+    raise ValueError(name)
