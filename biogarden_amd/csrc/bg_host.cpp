@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "bg_device.h"
+#include "bg_host_passes.h"
 #include "biogarden_gpu.h"
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
@@ -48,6 +49,10 @@ extern "C" size_t bg_finish_ack_lds_bytes(int R, int K, int local, int nslots, i
 #include "bg_tables.inc"
 
 namespace {
+
+using bgh::HScore;
+using bgh::host_threads;
+using bgh::par_ranges;
 
 struct DevBuf {
   void* p = nullptr;
@@ -94,134 +99,6 @@ struct PinBuf {
 };
 
 inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
-
-// CPUs this process may run on: its affinity mask, bounded by the cgroup's CPU quota (threads
-// beyond the quota only time-share it, and a burst over it is throttled for the rest of the
-// scheduler period).  The MI355X boxes show 256 CPUs with a 16-CPU quota per GPU.
-int usable_cpus() {
-  static const int n = [] {
-    int c = (int)std::thread::hardware_concurrency();
-    cpu_set_t set;
-    if (sched_getaffinity(0, sizeof(set), &set) == 0) c = CPU_COUNT(&set);
-    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
-      char q[32] = {0};
-      long per = 0;
-      if (std::fscanf(f, "%31s %ld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0)
-        c = std::min(c, std::max(1, (int)(std::atol(q) / per)));
-      std::fclose(f);
-    }
-    return std::max(1, c);
-  }();
-  return n;
-}
-
-// Host threads for the byte passes of prepare / fetch: at most 16 (a GPU's share of the host's
-// cores on the MI355X nodes) and the usable CPUs, one per ~256 KiB of input; BG_HOST_THREADS
-// overrides.
-int host_threads(uint64_t bytes) {
-  int t = std::min(16, usable_cpus());
-  if (const char* e = std::getenv("BG_HOST_THREADS")) t = std::max(1, std::atoi(e));
-  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)t, bytes / (256 << 10) + 1));
-}
-
-// A persistent pool of host worker threads for the byte passes (created once, reused by every
-// handle): a parallel region costs two condition-variable hand-offs instead of a thread
-// creation and join per worker per call (16 of them per prepare and per fetch, ~1 ms a batch on
-// the streaming path).  One region at a time; the calling thread takes a share of the tasks.
-class HostPool {
- public:
-  static HostPool& get() {
-    static HostPool* p = new HostPool();   // never destroyed: workers may outlive static dtors
-    return *p;
-  }
-  // runs f(0) .. f(n - 1), at most one task per thread at a time, returns when all are done
-  template <class F>
-  void run(int n, const F& f) {
-    if (n <= 1) { if (n == 1) f(0); return; }
-    std::lock_guard<std::mutex> region(callM_);
-    const int want = n - 1;
-    {
-      std::lock_guard<std::mutex> g(m_);
-      while ((int)th_.size() < want) th_.emplace_back([this] { worker(); });
-      task_ = [&f](int k) { f(k); };
-      ntasks_ = n;
-      next_ = 0;
-      finished_ = 0;
-      ++gen_;
-    }
-    cv_.notify_all();
-    drain();
-    std::unique_lock<std::mutex> lk(m_);
-    done_.wait(lk, [this] { return finished_ == ntasks_; });
-    task_ = nullptr;
-  }
-
- private:
-  void drain() {
-    for (;;) {
-      int k;
-      {
-        std::lock_guard<std::mutex> g(m_);
-        if (next_ >= ntasks_) return;
-        k = next_++;
-      }
-      task_(k);
-      std::lock_guard<std::mutex> g(m_);
-      if (++finished_ == ntasks_) done_.notify_all();
-    }
-  }
-  void worker() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> lk(m_);
-        cv_.wait(lk, [&] { return gen_ != seen; });
-        seen = gen_;
-      }
-      drain();
-    }
-  }
-  std::mutex callM_, m_;
-  std::condition_variable cv_, done_;
-  std::vector<std::thread> th_;
-  std::function<void(int)> task_;
-  int ntasks_ = 0, next_ = 0, finished_ = 0;
-  uint64_t gen_ = 0;
-};
-
-// Runs fn(lo, hi) over [0, n) split into contiguous ranges of about equal weight
-// (weight(i) = bytes of item i), one per pool task; inline when one thread suffices.
-template <class Wt, class F>
-void par_ranges(size_t n, Wt weight, F fn) {
-  uint64_t total = 0;
-  for (size_t i = 0; i < n; ++i) total += weight(i);
-  const int T = host_threads(total);
-  if (T <= 1 || n < 2) { fn((size_t)0, n); return; }
-  std::vector<size_t> cut(1, 0);
-  size_t lo = 0;
-  uint64_t acc = 0;
-  for (int k = 0; k < T && lo < n; ++k) {
-    const uint64_t goal = total * (uint64_t)(k + 1) / (uint64_t)T;
-    size_t hi = lo;
-    while (hi < n && (acc < goal || hi == lo)) acc += weight(hi++);
-    if (k == T - 1) hi = n;
-    cut.push_back(hi);
-    lo = hi;
-  }
-  if (cut.back() < n) cut.back() = n;
-  HostPool::get().run((int)cut.size() - 1, [&](int k) { fn(cut[k], cut[k + 1]); });
-}
-
-// The score closure tabulated over the codes a batch may use: code[byte] (0xFFFF:
-// the closure panics on that byte, score.rs:40), tab[q * K + c].  The 32 x 32 bg_scoring and the
-// wide table of bg_batch_prepare_table (up to 256 codes: any byte alphabet, as the reference's
-// &dyn Fn(&u8, &u8) -> i32 and analysis::seq's raw-byte equality allow) both become this.
-struct HScore {
-  uint16_t code[256];
-  int K = 0;
-  std::vector<int32_t> tab;
-  int32_t at(int q, int c) const { return tab[(size_t)q * K + c]; }
-};
 
 // Host-side phases of prepare / fetch, accumulated per handle (bg_host_timing) and, with
 // BG_PREPARE_TIMING set, printed per call on stderr
@@ -780,7 +657,6 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   h->npairs = npairs;
   h->n1v.assign(n1, n1 + npairs);
   h->n2v.assign(n2, n2 + npairs);
-  h->prestatus.assign(npairs, -1);
   h->outoff.resize(npairs);
   uint64_t off = 0;
   for (size_t p = 0; p < npairs; ++p) {
@@ -789,88 +665,19 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   }
   h->outBytes = off;
 
-  // ---- per-pair validation, in the reference's order
-  const bool needNonPos = mode == BG_GLOBAL || mode == BG_LOCAL || mode == BG_FITTING;
-  std::vector<char> present(S.K, 0);
-  for (size_t p = 0; p < npairs; ++p) {
-    if ((n1[p] && !s1[p]) || (n2[p] && !s2[p])) return BG_E_ARG;
-    if (n1[p] > 0x3FFFFFFF || n2[p] > 0x3FFFFFFF) return BG_E_ARG;
-    if (needNonPos && (a > 0 || b > 0)) { h->prestatus[p] = BG_INVALID_ARGUMENT_RANGE; continue; }
-    if (mode == BG_FITTING && n1[p] < n2[p]) { h->prestatus[p] = BG_INVALID_INPUT_SIZE; continue; }
-  }
-  // the score closure's domain (score.rs:38-41 panics outside it): per pair, the set of codes its
-  // residues use, 0 bit 31 reserved for "a byte with no code" — one table lookup and OR per byte,
-  // pairs split over host threads by bytes
-  uint32_t bitOf[256];
-  for (int x = 0; x < 256; ++x) {
-    const uint16_t c = S.code[x];
-    bitOf[x] = (c < 32 && c < S.K) ? (1u << c) : 0x80000000u;
-  }
-  bool codeBad = false;                 // a byte coded 31 collides with the marker: scan exactly
-  for (int x = 0; x < 256; ++x) codeBad |= S.code[x] == 31;
-  const bool wideK = S.K > 32;          // codes beyond 31: 256-bit sets per pair
-  h->pmask.assign(npairs, 0);
-  if (wideK) h->pmaskW.assign(npairs * 4, 0);
-  // the raw residues go to pinned staging in caller order in the same pass (the plan's LPT
-  // order only permutes BgPair records, never the bytes): one read of the caller's buffers
-  h->coff1.resize(npairs + 1);
-  h->coff2.resize(npairs + 1);
-  h->coff1[0] = h->coff2[0] = 0;
-  for (size_t p = 0; p < npairs; ++p) {
-    const bool stage = h->prestatus[p] < 0;
-    h->coff1[p + 1] = h->coff1[p] + (stage ? n1[p] : 0);
-    h->coff2[p + 1] = h->coff2[p] + (stage ? n2[p] : 0);
-  }
+  // ---- per-pair validation, in the reference's order, and the staging pass (bg_host_passes.h):
+  // the raw residues go to pinned staging in caller order (the plan's LPT order only permutes
+  // BgPair records, never the bytes), with each pair's score-code set, in one read of the
+  // caller's buffers
+  if (bgh::stage_validate(mode, npairs, s1, n1, s2, n2, a, b, h->prestatus, h->coff1, h->coff2))
+    return BG_E_ARG;
   const uint64_t o1 = h->coff1[npairs], o2 = h->coff2[npairs];
   if (!h->up.ensure(o1 + o2 + 512)) return BG_E_NOMEM;
   uint8_t* st1 = h->up.as<uint8_t>();
   uint8_t* st2 = st1 + o1 + 16;
-  par_ranges(npairs, [&](size_t p) -> uint64_t { return (uint64_t)n1[p] + n2[p]; },
-             [&](size_t lo, size_t hi) {
-    for (size_t p = lo; p < hi; ++p) {
-      if (h->prestatus[p] >= 0) continue;
-      if (n1[p]) std::memcpy(st1 + h->coff1[p], s1[p], n1[p]);
-      if (n2[p]) std::memcpy(st2 + h->coff2[p], s2[p], n2[p]);
-      if (n1[p] == 0 || n2[p] == 0) continue;   // the score closure is never called
-      const uint8_t* x1 = st1 + h->coff1[p];
-      const uint8_t* x2 = st2 + h->coff2[p];
-      bool bad = false;
-      if (wideK) {
-        uint64_t m4[4] = {0, 0, 0, 0};
-        for (int side = 0; side < 2 && !bad; ++side) {
-          const uint8_t* x = side ? x2 : x1;
-          const size_t n = side ? n2[p] : n1[p];
-          for (size_t i = 0; i < n; ++i) {
-            const uint16_t c = S.code[x[i]];
-            if (c >= S.K) { bad = true; break; }
-            m4[c >> 6] |= 1ull << (c & 63);
-          }
-        }
-        if (bad) h->prestatus[p] = BG_UNSCORABLE;
-        else for (int w = 0; w < 4; ++w) h->pmaskW[p * 4 + w] = m4[w];
-        continue;
-      }
-      uint32_t m = 0;
-      for (size_t i = 0; i < n1[p]; ++i) m |= bitOf[x1[i]];
-      for (size_t j = 0; j < n2[p]; ++j) m |= bitOf[x2[j]];
-      if (codeBad) {
-        for (size_t i = 0; i < n1[p] && !bad; ++i) bad = S.code[x1[i]] >= 32 || S.code[x1[i]] >= S.K;
-        for (size_t j = 0; j < n2[p] && !bad; ++j) bad = S.code[x2[j]] >= 32 || S.code[x2[j]] >= S.K;
-      } else {
-        bad = (m & 0x80000000u) != 0;
-      }
-      if (bad) h->prestatus[p] = BG_UNSCORABLE;
-      else h->pmask[p] = m;
-    }
-  });
-  for (size_t p = 0; p < npairs; ++p) {
-    if (h->prestatus[p] >= 0) continue;
-    if (wideK) {
-      for (int c = 0; c < S.K; ++c) present[c] |= ((h->pmaskW[p * 4 + (c >> 6)] >> (c & 63)) & 1u) != 0;
-    } else {
-      for (int c = 0; c < 32 && c < S.K; ++c) present[c] |= ((h->pmask[p] >> c) & 1u) != 0;
-    }
-  }
+  std::vector<char> present;
+  bgh::stage_copy(npairs, s1, n1, s2, n2, S, h->prestatus, h->coff1, h->coff2, st1, st2, h->pmask,
+                  h->pmaskW, present);
 
   tm.mark(kPhStage, "validate+stage");
   // ---- the reference's scratch history over the batch's calls (aligner.rs:92-94): the
@@ -878,18 +685,9 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   // resizes first.  Edit distance and LCS do not use a SequenceAligner.
   // A shard's calls may start from dims given per pair (bg_aligner_set_call_dims): the history
   // of the whole batch, replayed by the caller; the dims after the shard follow its last call.
-  const bool given = !callDims.empty();
-  if (given && callDims.size() != npairs) return BG_E_ARG;
+  if (!callDims.empty() && callDims.size() != npairs) return BG_E_ARG;
   long bufR = h->bufRows, bufC = h->bufCols;
-  h->bufAt.assign(npairs, std::make_pair(bufR, bufC));
-  for (size_t p = 0; p < npairs; ++p) {
-    if (given) { bufR = callDims[p].first; bufC = callDims[p].second; }
-    h->bufAt[p] = std::make_pair(bufR, bufC);
-    if (h->finFlags || h->prestatus[p] == BG_INVALID_ARGUMENT_RANGE ||
-        h->prestatus[p] == BG_INVALID_INPUT_SIZE)
-      continue;
-    if ((long)n1[p] > bufR || (long)n2[p] > bufC) { bufR = (long)n1[p] + 1; bufC = (long)n2[p] + 1; }
-  }
+  bgh::call_history(npairs, n1, n2, h->prestatus, callDims, h->finFlags != 0, bufR, bufC, h->bufAt);
 
   // ---- dense alphabet, profile, kernel family
   const int KS = S.K;
@@ -1453,29 +1251,25 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
     const BgResult& r = h->hres[q];
     if (r.out_len > (uint32_t)(P.n1 + P.n2) || r.out_start + r.out_len > (uint32_t)(P.n1 + P.n2)) return BG_E_HIP;
   }
-  const uint8_t* h1 = h->ho1.as<uint8_t>();
-  const uint8_t* h2 = h->ho2.as<uint8_t>();
-  par_ranges(np, [&](size_t q) -> uint64_t { return 2ull * h->hres[q].out_len + 64; },
-             [&](size_t lo, size_t hi) {
-    for (size_t q = lo; q < hi; ++q) {
-      const BgPair& P = h->plan[q];
-      const BgResult& r = h->hres[q];
-      const size_t p = h->order_[q];
-      bg_pair_result& o = res[p];
-      o.status = r.status;
-      o.score = r.score;
-      o.len = r.out_len;
-      o.end_i = (uint32_t)r.end_i;
-      o.end_j = (uint32_t)r.end_j;
-      o.start1 = r.start1;
-      o.start2 = r.start2;
-      std::memcpy(out1 + h->outoff[p], h1 + P.out_off + r.out_start, r.out_len);
-      std::memcpy(out2 + h->outoff[p], h2 + P.out_off + r.out_start, r.out_len);
-      if (o.status == BG_OK && bg_ref_divergent(h->mode, (long)h->n1v[p], (long)h->n2v[p], r.score,
-                                                h->bufAt[p].first, h->bufAt[p].second))
-        o.status = BG_REF_DIVERGENT;
-    }
-  });
+  std::vector<bgh::UnpackJob> jobs(np);
+  for (size_t q = 0; q < np; ++q) {
+    const BgPair& P = h->plan[q];
+    const BgResult& r = h->hres[q];
+    const size_t p = h->order_[q];
+    bg_pair_result& o = res[p];
+    o.status = r.status;
+    o.score = r.score;
+    o.len = r.out_len;
+    o.end_i = (uint32_t)r.end_i;
+    o.end_j = (uint32_t)r.end_j;
+    o.start1 = r.start1;
+    o.start2 = r.start2;
+    if (o.status == BG_OK && bg_ref_divergent(h->mode, (long)h->n1v[p], (long)h->n2v[p], r.score,
+                                              h->bufAt[p].first, h->bufAt[p].second))
+      o.status = BG_REF_DIVERGENT;
+    jobs[q] = bgh::UnpackJob{P.out_off + r.out_start, h->outoff[p], r.out_len};
+  }
+  bgh::unpack_strings(jobs, h->ho1.as<uint8_t>(), h->ho2.as<uint8_t>(), out1, out2);
   tm.mark(kPhFetchUnpack, "fetch-unpack");
   return BG_OK;
 }

@@ -1,0 +1,293 @@
+// Host-side byte passes behind the C ABI (bg_host.cpp): validation and staging of a batch's
+// residues, the reference aligner's scratch history, and the unpacking of fetched strings, with
+// the worker pool they run on.  Plain C++17 with no HIP dependency, so the pointer and offset
+// arithmetic can be exercised under AddressSanitizer / UBSan on a CPU-only host
+// (tests/cpp/test_host_passes.cpp, tests/test_sanitizers.py).
+//
+// Reference behaviour mirrored here:
+//   argument checks      aligner.rs:87-89, 153-155, 219-225 (status 1 / 2, in that order)
+//   score closure domain score.rs:38-41 (a byte outside the table panics: status 3)
+//   scratch history      aligner.rs:92-94, 594-602 (resize to (n1+1, n2+1) iff n1 > rows || n2 > cols)
+#pragma once
+#include <sched.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <utility>
+#include <vector>
+
+#include "biogarden_gpu.h"
+
+namespace bgh {
+
+// CPUs this process may run on: its affinity mask, bounded by the cgroup's CPU quota (threads
+// beyond the quota only time-share it, and a burst over it is throttled for the rest of the
+// scheduler period).  The MI355X boxes show 256 CPUs with a 16-CPU quota per GPU.
+inline int usable_cpus() {
+  static const int n = [] {
+    int c = (int)std::thread::hardware_concurrency();
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) c = CPU_COUNT(&set);
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char q[32] = {0};
+      long per = 0;
+      if (std::fscanf(f, "%31s %ld", q, &per) == 2 && std::strcmp(q, "max") != 0 && per > 0)
+        c = std::min(c, std::max(1, (int)(std::atol(q) / per)));
+      std::fclose(f);
+    }
+    return std::max(1, c);
+  }();
+  return n;
+}
+
+// Host threads for the byte passes of prepare / fetch: at most 16 (a GPU's share of the host's
+// cores on the MI355X nodes) and the usable CPUs, one per ~256 KiB of input; BG_HOST_THREADS
+// overrides.
+inline int host_threads(uint64_t bytes) {
+  int t = std::min(16, usable_cpus());
+  if (const char* e = std::getenv("BG_HOST_THREADS")) t = std::max(1, std::atoi(e));
+  return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)t, bytes / (256 << 10) + 1));
+}
+
+// A persistent pool of host worker threads for the byte passes (created once, reused by every
+// handle): a parallel region costs two condition-variable hand-offs instead of a thread
+// creation and join per worker per call (16 of them per prepare and per fetch, ~1 ms a batch on
+// the streaming path).  One region at a time; the calling thread takes a share of the tasks.
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool();   // never destroyed: workers may outlive static dtors
+    return *p;
+  }
+  // runs f(0) .. f(n - 1), at most one task per thread at a time, returns when all are done
+  template <class F>
+  void run(int n, const F& f) {
+    if (n <= 1) { if (n == 1) f(0); return; }
+    std::lock_guard<std::mutex> region(callM_);
+    const int want = n - 1;
+    {
+      std::lock_guard<std::mutex> g(m_);
+      while ((int)th_.size() < want) th_.emplace_back([this] { worker(); });
+      task_ = [&f](int k) { f(k); };
+      ntasks_ = n;
+      next_ = 0;
+      finished_ = 0;
+      ++gen_;
+    }
+    cv_.notify_all();
+    drain();
+    std::unique_lock<std::mutex> lk(m_);
+    done_.wait(lk, [this] { return finished_ == ntasks_; });
+    task_ = nullptr;
+  }
+
+ private:
+  void drain() {
+    for (;;) {
+      int k;
+      {
+        std::lock_guard<std::mutex> g(m_);
+        if (next_ >= ntasks_) return;
+        k = next_++;
+      }
+      task_(k);
+      std::lock_guard<std::mutex> g(m_);
+      if (++finished_ == ntasks_) done_.notify_all();
+    }
+  }
+  void worker() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+      }
+      drain();
+    }
+  }
+  std::mutex callM_, m_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> th_;
+  std::function<void(int)> task_;
+  int ntasks_ = 0, next_ = 0, finished_ = 0;
+  uint64_t gen_ = 0;
+};
+
+// Runs fn(lo, hi) over [0, n) split into contiguous ranges of about equal weight
+// (weight(i) = bytes of item i), one per pool task; inline when one thread suffices.
+template <class Wt, class F>
+void par_ranges(size_t n, Wt weight, F fn) {
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) total += weight(i);
+  const int T = host_threads(total);
+  if (T <= 1 || n < 2) { fn((size_t)0, n); return; }
+  std::vector<size_t> cut(1, 0);
+  size_t lo = 0;
+  uint64_t acc = 0;
+  for (int k = 0; k < T && lo < n; ++k) {
+    const uint64_t goal = total * (uint64_t)(k + 1) / (uint64_t)T;
+    size_t hi = lo;
+    while (hi < n && (acc < goal || hi == lo)) acc += weight(hi++);
+    if (k == T - 1) hi = n;
+    cut.push_back(hi);
+    lo = hi;
+  }
+  if (cut.back() < n) cut.back() = n;
+  HostPool::get().run((int)cut.size() - 1, [&](int k) { fn(cut[k], cut[k + 1]); });
+}
+
+// The score closure tabulated over the codes a batch may use: code[byte] (0xFFFF:
+// the closure panics on that byte, score.rs:40), tab[q * K + c].  The 32 x 32 bg_scoring and the
+// wide table of bg_batch_prepare_table (up to 256 codes: any byte alphabet, as the reference's
+// &dyn Fn(&u8, &u8) -> i32 and analysis::seq's raw-byte equality allow) both become this.
+struct HScore {
+  uint16_t code[256];
+  int K = 0;
+  std::vector<int32_t> tab;
+  int32_t at(int q, int c) const { return tab[(size_t)q * K + c]; }
+};
+
+// ---- prepare, part 1: per-pair argument checks in the reference's order (status 1 before 2),
+// and the caller-order offsets of the residues that will be staged (pairs with a status are not).
+// Returns BG_OK or BG_E_ARG (a null pointer with a nonzero length, a length beyond 2^30 - 1).
+inline int stage_validate(int mode, size_t npairs, const uint8_t* const* s1, const size_t* n1,
+                          const uint8_t* const* s2, const size_t* n2, int32_t a, int32_t b,
+                          std::vector<int>& prestatus, std::vector<uint64_t>& coff1,
+                          std::vector<uint64_t>& coff2) {
+  const bool needNonPos = mode == BG_GLOBAL || mode == BG_LOCAL || mode == BG_FITTING;
+  prestatus.assign(npairs, -1);
+  for (size_t p = 0; p < npairs; ++p) {
+    if ((n1[p] && !s1[p]) || (n2[p] && !s2[p])) return BG_E_ARG;
+    if (n1[p] > 0x3FFFFFFF || n2[p] > 0x3FFFFFFF) return BG_E_ARG;
+    if (needNonPos && (a > 0 || b > 0)) { prestatus[p] = BG_INVALID_ARGUMENT_RANGE; continue; }
+    if (mode == BG_FITTING && n1[p] < n2[p]) { prestatus[p] = BG_INVALID_INPUT_SIZE; continue; }
+  }
+  coff1.resize(npairs + 1);
+  coff2.resize(npairs + 1);
+  coff1[0] = coff2[0] = 0;
+  for (size_t p = 0; p < npairs; ++p) {
+    const bool stage = prestatus[p] < 0;
+    coff1[p + 1] = coff1[p] + (stage ? n1[p] : 0);
+    coff2[p + 1] = coff2[p] + (stage ? n2[p] : 0);
+  }
+  return BG_OK;
+}
+
+// ---- prepare, part 2: one pass over the caller's bytes, split over the pool by bytes: the raw
+// residues of every pair without a status go to st1 / st2 at coff1 / coff2 (caller order), and
+// each such pair's set of score codes is computed — pmask (codes < 32; bit 31 marks a byte the
+// closure panics on) or, for alphabets beyond 32 codes, pmaskW (4 x 64 bits per pair).  A pair
+// touching an unscorable byte gets status 3 (score.rs:40 panics; never for an empty side: the
+// closure is not called).  present[c] = some staged pair uses code c.
+inline void stage_copy(size_t npairs, const uint8_t* const* s1, const size_t* n1,
+                       const uint8_t* const* s2, const size_t* n2, const HScore& S,
+                       std::vector<int>& prestatus, const std::vector<uint64_t>& coff1,
+                       const std::vector<uint64_t>& coff2, uint8_t* st1, uint8_t* st2,
+                       std::vector<uint32_t>& pmask, std::vector<uint64_t>& pmaskW,
+                       std::vector<char>& present) {
+  uint32_t bitOf[256];
+  for (int x = 0; x < 256; ++x) {
+    const uint16_t c = S.code[x];
+    bitOf[x] = (c < 32 && c < S.K) ? (1u << c) : 0x80000000u;
+  }
+  bool codeBad = false;                 // a byte coded 31 collides with the marker: scan exactly
+  for (int x = 0; x < 256; ++x) codeBad |= S.code[x] == 31;
+  const bool wideK = S.K > 32;          // codes beyond 31: 256-bit sets per pair
+  pmask.assign(npairs, 0);
+  if (wideK) pmaskW.assign(npairs * 4, 0);
+  present.assign(S.K, 0);
+  par_ranges(npairs, [&](size_t p) -> uint64_t { return (uint64_t)n1[p] + n2[p]; },
+             [&](size_t lo, size_t hi) {
+    for (size_t p = lo; p < hi; ++p) {
+      if (prestatus[p] >= 0) continue;
+      if (n1[p]) std::memcpy(st1 + coff1[p], s1[p], n1[p]);
+      if (n2[p]) std::memcpy(st2 + coff2[p], s2[p], n2[p]);
+      if (n1[p] == 0 || n2[p] == 0) continue;   // the score closure is never called
+      const uint8_t* x1 = st1 + coff1[p];
+      const uint8_t* x2 = st2 + coff2[p];
+      bool bad = false;
+      if (wideK) {
+        uint64_t m4[4] = {0, 0, 0, 0};
+        for (int side = 0; side < 2 && !bad; ++side) {
+          const uint8_t* x = side ? x2 : x1;
+          const size_t n = side ? n2[p] : n1[p];
+          for (size_t i = 0; i < n; ++i) {
+            const uint16_t c = S.code[x[i]];
+            if (c >= S.K) { bad = true; break; }
+            m4[c >> 6] |= 1ull << (c & 63);
+          }
+        }
+        if (bad) prestatus[p] = BG_UNSCORABLE;
+        else for (int w = 0; w < 4; ++w) pmaskW[p * 4 + w] = m4[w];
+        continue;
+      }
+      uint32_t m = 0;
+      for (size_t i = 0; i < n1[p]; ++i) m |= bitOf[x1[i]];
+      for (size_t j = 0; j < n2[p]; ++j) m |= bitOf[x2[j]];
+      if (codeBad) {
+        for (size_t i = 0; i < n1[p] && !bad; ++i) bad = S.code[x1[i]] >= 32 || S.code[x1[i]] >= S.K;
+        for (size_t j = 0; j < n2[p] && !bad; ++j) bad = S.code[x2[j]] >= 32 || S.code[x2[j]] >= S.K;
+      } else {
+        bad = (m & 0x80000000u) != 0;
+      }
+      if (bad) prestatus[p] = BG_UNSCORABLE;
+      else pmask[p] = m;
+    }
+  });
+  for (size_t p = 0; p < npairs; ++p) {
+    if (prestatus[p] >= 0) continue;
+    if (wideK) {
+      for (int c = 0; c < S.K; ++c) present[c] |= ((pmaskW[p * 4 + (c >> 6)] >> (c & 63)) & 1u) != 0;
+    } else {
+      for (int c = 0; c < 32 && c < S.K; ++c) present[c] |= ((pmask[p] >> c) & 1u) != 0;
+    }
+  }
+}
+
+// ---- the reference's scratch history over a batch's calls (aligner.rs:92-94): bufAt[p] = the
+// dims call p starts from.  The argument errors return before the resize; everything else (the
+// score panic included) resizes first.  `given` (npairs entries, or empty): per-pair start dims
+// of a shard (bg_aligner_set_call_dims).  `noAligner` (edit distance, LCS): no history.
+// Updates rows / cols to the dims after the last call.
+inline void call_history(size_t npairs, const size_t* n1, const size_t* n2,
+                         const std::vector<int>& prestatus,
+                         const std::vector<std::pair<long, long>>& given, bool noAligner,
+                         long& rows, long& cols, std::vector<std::pair<long, long>>& bufAt) {
+  bufAt.assign(npairs, std::make_pair(rows, cols));
+  for (size_t p = 0; p < npairs; ++p) {
+    if (!given.empty()) { rows = given[p].first; cols = given[p].second; }
+    bufAt[p] = std::make_pair(rows, cols);
+    if (noAligner || prestatus[p] == BG_INVALID_ARGUMENT_RANGE || prestatus[p] == BG_INVALID_INPUT_SIZE)
+      continue;
+    if ((long)n1[p] > rows || (long)n2[p] > cols) { rows = (long)n1[p] + 1; cols = (long)n2[p] + 1; }
+  }
+}
+
+// ---- fetch: copy each pair's aligned strings from the downloaded slot buffers to the caller's
+// output, over the pool: job q copies len bytes at src of h1 / h2 to dst of out1 / out2.
+struct UnpackJob {
+  uint64_t src, dst;
+  uint32_t len;
+};
+inline void unpack_strings(const std::vector<UnpackJob>& jobs, const uint8_t* h1, const uint8_t* h2,
+                           uint8_t* out1, uint8_t* out2) {
+  par_ranges(jobs.size(), [&](size_t q) -> uint64_t { return 2ull * jobs[q].len + 64; },
+             [&](size_t lo, size_t hi) {
+    for (size_t q = lo; q < hi; ++q) {
+      const UnpackJob& j = jobs[q];
+      if (!j.len) continue;
+      std::memcpy(out1 + j.dst, h1 + j.src, j.len);
+      std::memcpy(out2 + j.dst, h2 + j.src, j.len);
+    }
+  });
+}
+
+}  // namespace bgh

@@ -245,7 +245,7 @@ int bg_lcs_batch(bg_aligner* h, size_t npairs, const uint8_t* const* s1, const s
 typedef struct bg_fasta bg_fasta;
 typedef struct bg_fasta_batch {
   size_t n;                    /* records in this batch (0: the file is exhausted) */
-  const uint8_t* seq;
+  const uint8_t* seq;          /* NULL allowed when the batch holds no residues */
   const uint64_t* seq_off;     /* n + 1 entries */
   const char* text;
   const uint64_t* id_off;      /* n entries */

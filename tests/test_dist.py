@@ -107,6 +107,102 @@ def _sharded_worker(rank, world, port, q, mode, a, b):
         dist.destroy_process_group()
 
 
+def _faithful_results(pairs, mode, a, b, dims):
+    """What a rank's fetch returns for its shard when every call starts from the scratch dims a
+    single reference aligner would hold (shard.call_dims): the reference-faithful oracle from
+    those dims (status 4 where it panics or its answer differs from the exact-size one)."""
+    from oracle import refcpu
+    out = []
+    for (s1, s2), d in zip(pairs, dims):
+        st, sc, o1, o2 = refcpu.align(mode, s1, s2, "blosum62", a, b, exact=True)
+        fst, fsc, f1, f2 = refcpu.Aligner(dims=d).align(mode, s1, s2, "blosum62", a, b)
+        if st == 0 and not (fst == 0 and (fsc, f1, f2) == (sc, o1, o2)):
+            st = 4
+        out.append({"status": st, "score": sc, "aligned1": o1, "aligned2": o2,
+                    "end": (len(s1), len(s2)), "start": (0, 0)})
+    return out
+
+
+def _c4_like_pairs():
+    """C4's shape (150 bp reads with 2 % substitutions against 10 kbp refs, seq1 = read) plus
+    calls whose statuses depend on the batch's history: after a 1100 x 1100 call resized the
+    scratch to 1101 x 1101, a 1101-long seq1 and a 1101-long seq2 (equal to the rows / columns:
+    the reference panics, aligner.rs:92-94) and a 1099 x 700 one (it does not)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from tools import workloads
+    pairs = workloads.c4_pairs(nrefs=2, reads_per_ref=6)
+    rng = random.Random(5)
+    seq = lambda n: bytes(rng.choice(b"ACGT") for _ in range(n))  # noqa: E731
+    pairs[3:3] = [(seq(1100), seq(1100)), (seq(1101), seq(700)), (seq(150), seq(1101)),
+                  (seq(1099), seq(700))]
+    return pairs
+
+
+def _c4_sharded_worker(rank, world, port, q):
+    """A C4-shaped batch through the multi-rank path with the whole batch's call history."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mode, a, b = "semiglobal", -1, -2
+        pairs = _c4_like_pairs()
+        sizes = [(len(x), len(y)) for x, y in pairs]
+        shards = shard.lpt_shards(sizes, world)
+        dims = shard.shard_call_dims(mode, sizes, a, b, shards[rank])
+        mine = _faithful_results([pairs[p] for p in shards[rank]], mode, a, b, dims)
+        local = torch.frombuffer(bytearray(shard.encode_export(mine)), dtype=torch.uint8)
+        got = shard.gather_packed(local, dist, dst=0)
+        if rank == 0:
+            merged = shard.merge_shards(shards, [_native.decode_export(x) for x in got])
+            single = _faithful_results(pairs, mode, a, b, shard.call_dims(mode, sizes, a, b))
+            # the sequential reference aligner over the whole batch, for the statuses
+            from oracle import refcpu
+            al = refcpu.Aligner(exact=False)
+            seq_st = []
+            for s1, s2 in pairs:
+                fst = al.align(mode, s1, s2, "blosum62", a, b)
+                seq_st.append(fst)
+            q.put(("ok", merged == single, [r["status"] for r in merged],
+                   [(f[0], f[1:]) for f in seq_st], [r["score"] for r in single],
+                   [(r["aligned1"], r["aligned2"]) for r in single]))
+        else:
+            q.put(("rank", rank, got is None))
+    except Exception as e:  # surface worker failures to the test
+        q.put(("err", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_c4_shaped_shards_equal_one_reference_aligner(world):
+    """C4-shaped pairs sharded over gloo ranks, each rank starting its calls from the whole
+    batch's scratch history: merged statuses, scores and strings equal ONE reference aligner
+    running the batch in order (status 4 exactly where that aligner panics or answers from
+    stale scratch)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_sharded_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+    ok = [m for m in msgs if m[0] == "ok"]
+    assert len(ok) == 1, msgs
+    _, same, statuses, seq, scores, strings = ok[0]
+    assert same
+    for st, (fst, (fsc, f1, f2)), sc, (o1, o2) in zip(statuses, seq, scores, strings):
+        if fst == 0 and (fsc, f1, f2) == (sc, o1, o2):
+            assert st == 0
+        else:
+            assert st == 4
+    assert statuses[4] == 4 and statuses[5] == 4 and statuses[6] == 0, statuses
+    assert all(p.exitcode == 0 for p in procs)
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_sharded_batch_equals_single_rank(world):
     """The multi-rank data path on CPU ranks: the merged gather of every rank's packed shard

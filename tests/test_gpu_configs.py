@@ -135,6 +135,24 @@ def test_C3_wide_20k_string_parity(aligner, oracle):
     assert res[0].status == 0
 
 
+# ------------------------------------------------------------------ M: the metric's own batch
+
+
+def test_M_metric_batch_at_bench_geometry(aligner, oracle):
+    """bench.py's metric batch exactly (256 x 10 kbp x 10 kbp uniform DNA, semiglobal blosum62
+    -1/-2, rank 0's seed) through the default planner, which must pick the bench's geometry
+    (R = 8, W = 16, checkpoint traceback with 4-wave finish workgroups); score and both strings of
+    five pairs spread over the LPT order against the oracle, every status 0."""
+    w = _w()
+    pairs = w.metric_pairs(256)          # = bench.make_pairs(256, 10000, 10000, SEED) at rank 0
+    res = check_batch(aligner, oracle, "semiglobal", pairs, "blosum62", -1, -2,
+                      sample=[0, 63, 128, 200, 255])
+    st = aligner.stats()
+    assert (st["R"], st["waves"], st["tagged"], st["checkpoint"], st["wide"]) == (8, 16, 1, 1, 0), st
+    assert (st["fin_waves"], st["fin_slots"]) == (4, 0), st
+    assert all(r.status == 0 for r in res)
+
+
 # ------------------------------------------------------------------ MA: a < b at the metric shape
 
 
