@@ -22,7 +22,7 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
            "bg_set_pipeline", "bg_set_kernel_options", "bg_edit_distance_batch",
            "bg_lcs_batch", "bg_aligner_buffer_size", "bg_aligner_set_buffer_size",
-           "bg_aligner_set_call_dims", "bg_host_timing", "bg_fasta_open",
+           "bg_aligner_set_call_dims", "bg_host_timing", "bg_last_hip_error", "bg_fasta_open",
            "bg_batch_prepare_table", "bg_fasta_next_batch",
            "bg_fasta_close"]
 
@@ -159,7 +159,10 @@ def builtin_scoring(which):
 
 def check(rc):
     if rc < 0:
-        raise RuntimeError("biogarden_gpu: %s (%d)" % (lib().bg_status_string(rc).decode(), rc))
+        msg = "biogarden_gpu: %s (%d)" % (lib().bg_status_string(rc).decode(), rc)
+        if rc == -2:
+            msg += ", hipError_t %d" % lib().bg_last_hip_error()
+        raise RuntimeError(msg)
     return rc
 
 

@@ -15,6 +15,15 @@
 #ifndef BG_HELP_FAST
 #define BG_HELP_FAST 4
 #endif
+#ifndef BG_FIN_DEBUG
+#define BG_FIN_DEBUG 0     // range checks with printf in the traceback (diagnosis builds)
+#endif
+#ifndef BG_NO_SEQCHECK
+#define BG_NO_SEQCHECK 0   // experiment: skip the walker's post-decode slot check
+#endif
+#ifndef BG_FIN_WAKEUP
+#define BG_FIN_WAKEUP 0
+#endif
 #ifndef BG_HELP_LONG
 #define BG_HELP_LONG 8
 #endif
@@ -410,9 +419,11 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     if constexpr (CK) {
       const int cc = t >> 6;
       // (s << 20 | c << 4 | slot); an atomic load: helper waves publish chunks concurrently
-      const unsigned e = __hip_atomic_load(&ckMap[ck_map_idx(sidx, cc)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const int mi = ck_map_idx(sidx, cc);
+      const unsigned e = __hip_atomic_load(&ckMap[mi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       if ((e >> 4) != (((unsigned)sidx << 16) | (unsigned)cc) || e == 0xFFFFFFFFu) return kCodeMiss;
       const int z = (int)(e & 15);
+      if (z >= nSlots) return kCodeMiss;                 // never published (guard)
       if constexpr (ACK) {
         // bit planes (aff_recomp): not-Y, not-X, x_trace 'I', y_trace 'I' [, local stop]
         constexpr int NP = ack_planes<MODE == BGK_LOCAL>();
@@ -457,7 +468,23 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       __hip_atomic_store(&sh[35], la, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     const u64 td0 = F.dbg ? __builtin_readcyclecounter() : 0;
-    codes = decode_cell(k0 - (lane >> 3), l0 - (lane & 7));
+    if (CK && asyncPos && !BG_NO_SEQCHECK) {
+      // Asynchronous recomputation: a helper may re-assign a slot while this decode reads it (it
+      // judged the walker's footprint from the position posted before this one, or the slot's
+      // map entry had been replaced by a colliding chunk).  Helpers bump the eviction epoch
+      // sh[59] when they claim a slot that held a chunk, before they write into it, and one
+      // wave's LDS operations complete in order: an epoch unchanged across the decode proves no
+      // slot it read was re-assigned meanwhile; otherwise decode again.
+      for (;;) {
+        const int e0 = __hip_atomic_load(&sh[59], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        codes = decode_cell(k0 - (lane >> 3), l0 - (lane & 7));
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (__hip_atomic_load(&sh[59], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == e0) break;
+      }
+    } else {
+      codes = decode_cell(k0 - (lane >> 3), l0 - (lane & 7));
+    }
     if (F.dbg) {
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       codes = __builtin_amdgcn_readfirstlane(0) + codes;
@@ -504,7 +531,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   asyncPos = async;
   if (async) {
     if (tid == 0) {
-      sh[32] = 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0; sh[37] = 0; sh[56] = -1;
+      sh[32] = 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0; sh[37] = 0; sh[56] = -1; sh[59] = 0;
       for (int z = 0; z < 8; ++z) { sh[40 + z] = -1; sh[48 + z] = 0; }
     }
     __syncthreads();
@@ -574,6 +601,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           if (oz >= 0) {
             unsigned& oe = ckMap[ck_map_idx(oz >> 16, oz & 0xffff)];
             if (oe == enc(oz, pick)) __hip_atomic_store(&oe, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            // the walker's decode check (reanchor): this slot is about to be overwritten
+            __hip_atomic_store(&sh[59], sh[59] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
           sh[40 + pick] = kk;
           sh[48 + pick] = 1;
@@ -582,8 +611,22 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         }
         __hip_atomic_store(&sh[36], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+      // the slot's old map entry was invalidated above, before any write into the slot below
+      // (one wave's LDS operations complete in order; keep the compiler from hoisting the
+      // recomputation's stores): the walker's post-decode check relies on that order
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
       key = uni(__shfl(key, 0, 64));
       zz = uni(__shfl(zz, 0, 64));
+      // keys come from mk() (range-checked) or the walker's miss, which lies inside the pair's
+      // strips and chunks; a key outside them would read beyond the pair's checkpoints
+      if (key >= 0 && ((key >> 16) >= NSp || (key & 0xffff) >= NCp || zz < 0 || zz >= nSlots)) {
+#if BG_FIN_DEBUG
+        if (lane == 0) printf("BGDBG pair %d: helper key (%d, %d) slot %d\n", P.index, key >> 16, key & 0xffff, zz);
+#endif
+        if (lane == 0 && zz >= 0 && zz < nSlots)
+          __hip_atomic_store(&sh[48 + zz], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        key = -1;
+      }
       if (key < 0) {
         // idle: nothing to recompute ahead of the walk.  Each poll takes the lock and scans the
         // candidates on a SIMD the next execute's DP waves share; after BG_HELP_FAST idle polls
@@ -648,6 +691,10 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             const int infoP = rdlane((ex ? 1 : 0) | (mv << 1), Pn);
             const int exP = infoP & 1, mvP = infoP >> 1;
             const int nops = Dn + exP;
+#if BG_FIN_DEBUG
+            if (lane == 0 && ntail + ncore + nops > cap)
+              printf("BGDBG pair %d: jumper writes op %d of cap %d at (%d, %d)\n", P.index, ntail + ncore + nops, cap, k, l);
+#endif
             if (lane < nops) ob[cap - 1 - (ntail + ncore + lane)] = (uint8_t)opx;
             ncore += nops;
             k -= Pn >> 3;
@@ -763,6 +810,11 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
               __hip_atomic_store(&sh[35], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               __hip_atomic_store(&sh[33], key, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
+#if BG_FIN_WAKEUP
+            // experiment (round 2's failing variant, re-created for diagnosis): wake the sleeping
+            // helpers of this workgroup right after posting the request
+            asm volatile("s_wakeup" ::: "memory");
+#endif
             const unsigned* me = &ckMap[ck_map_idx(reqS, reqB0)];
             // Forward progress: after kSelfPolls polls without a helper taking the request (all
             // busy prefetching), the walker claims a slot under the same lock and recomputes the
@@ -773,7 +825,13 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             bool got = false;
             for (;; ++it) {
               const unsigned e = __hip_atomic_load(me, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-              if (e != 0xFFFFFFFFu && (int)(e >> 4) == key) { got = true; break; }
+              if (e != 0xFFFFFFFFu && (int)(e >> 4) == key) {
+                // served: withdraw the request, so no helper recomputes it again once it has
+                // been evicted (a stale request may land on a map entry the walk is using)
+                if (lane == 0) __hip_atomic_store(&sh[33], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                got = true;
+                break;
+              }
               if (it >= selfPolls && (it - selfPolls) % 64 == 0) {
                 int zz = -1;
                 if (lane == 0) {
@@ -822,6 +880,11 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                   __hip_atomic_store(&sh[36], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
                 zz = uni(__shfl(zz, 0, 64));
+#if BG_FIN_DEBUG
+                if (zz >= 0 && (reqS < 0 || reqS >= P.nstrips || reqB0 < 0 || reqB0 >= P.nc || zz >= nSlots) && lane == 0)
+                  printf("BGDBG pair %d: self-serve key (%d, %d) slot %d of %d x %d / %d\n", P.index, reqS, reqB0, zz,
+                         P.nstrips, P.nc, nSlots);
+#endif
                 if (zz >= 0) {
                   recompute_chunk<R>(F, P, reqS, reqB0, win + (size_t)zz * kSlotDw, ckArea, lane);
                   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -857,6 +920,10 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         const int e = (int)(lut >> (4 * (c & 15))) & 15;
         const int mv = e >> 2;
         if ((mv == 2 && k == 0) || (mv == 3 && l == 0)) { status = 4; done = 1; break; }  // index underflow panic
+#if BG_FIN_DEBUG
+        if (lane == 0 && mv && ntail + ncore + 1 > cap)
+          printf("BGDBG pair %d: scalar walker writes op %d of cap %d at (%d, %d)\n", P.index, ntail + ncore + 1, cap, k, l);
+#endif
         k -= (0x6 >> mv) & 1;
         l -= (0xA >> mv) & 1;
         state = e & 3;
@@ -1011,8 +1078,27 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     __syncthreads();
   }
   int p1 = i0 + scan[tid] - c1, p2 = j0 + scan[NT + tid] - c2;
+#if BG_FIN_DEBUG
+  {
+    // the core's ops must consume exactly s1[kstop, kstop + ...) up to ei and s2 up to ej
+    const int tot1 = scan[NT - 1], tot2 = scan[2 * NT - 1];
+    if (tid == 0 && status != 5 && (i0 + tot1 != (colcase ? ei : (mode == BGK_SEMIGLOBAL ? ei : ei)) ||
+                                    j0 + tot2 != ej))
+      printf("BGDBG pair %d: ops consume (%d, %d) from (%d, %d), end (%d, %d), ncore %d ntail %d status %d\n",
+             P.index, tot1, tot2, i0, j0, ei, ej, ncore, ntail, status);
+    bool badop = false;
+    for (int x = lo; x < hi; ++x) badop |= ob[x] > 2;
+    if (badop) printf("BGDBG pair %d: op code > 2 in the core (tid %d)\n", P.index, tid);
+  }
+#endif
   for (int x = lo; x < hi; ++x) {
     const int op = ob[x];
+#if BG_FIN_DEBUG
+    if ((op != 2 && (p1 < 0 || p1 >= n1)) || (op != 1 && (p2 < 0 || p2 >= n2))) {
+      printf("BGDBG pair %d: expansion reads s1[%d] / s2[%d] of %d / %d (op %d)\n", P.index, p1, p2, n1, n2, op);
+      break;
+    }
+#endif
     const uint8_t ch1 = op != 2 ? f.s1[p1++] : (uint8_t)'-';
     const uint8_t ch2 = op != 1 ? f.s2[p2++] : (uint8_t)'-';
     ob[x] = ch1;

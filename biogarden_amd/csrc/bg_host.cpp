@@ -336,10 +336,24 @@ extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
   return BG_OK;
 }
 
-#define BG_HIP(x)                          \
-  do {                                     \
-    if ((x) != hipSuccess) return BG_E_HIP; \
+// A failing HIP call returns BG_E_HIP; its error name goes to stderr (the ABI's status codes have
+// no room for it) and to bg_last_hip_error().
+static thread_local int g_lastHip = 0;
+static void note_hip(hipError_t e, const char* what, int line) {
+  g_lastHip = (int)e;
+  std::fprintf(stderr, "biogarden_gpu: %s failed at bg_host.cpp:%d: %s (%d)\n", what, line,
+               hipGetErrorName(e), (int)e);
+}
+#define BG_HIP(x)                                              \
+  do {                                                         \
+    const hipError_t bg_e_ = (x);                              \
+    if (bg_e_ != hipSuccess) {                                 \
+      note_hip(bg_e_, #x, __LINE__);                           \
+      return BG_E_HIP;                                         \
+    }                                                          \
   } while (0)
+
+extern "C" int bg_last_hip_error(void) { return g_lastHip; }
 
 // Strip pipeline of one pair on `gw` waves: phases (64-step chunks) until its last strip ends.
 static int pipeline_phases(int S, int gw, int NC, int lag = 2) {

@@ -257,6 +257,10 @@ long bg_fasta_next_batch(bg_fasta* r, size_t max_records, size_t max_residues,
                                                                 maxima must be > 0 (BG_E_ARG) */
 void bg_fasta_close(bg_fasta* r);
 
+/* The hipError_t of the last HIP call that failed on this thread (BG_E_HIP), 0 if none; the
+ * failing call and the error's name are also printed on stderr. */
+int bg_last_hip_error(void);
+
 const char* bg_status_string(int status);
 int bg_abi_version(void);
 
