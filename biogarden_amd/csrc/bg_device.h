@@ -102,6 +102,7 @@ struct BgDpArgs {
   int32_t pstride;         // row stride of the int16 profile table (the batch's dense alphabet)
   unsigned long long* dbg; // optional per-wave timestamps of the first strip (env BG_DP_TIMING):
                            // [gw * 8 + k], k: 0 strip, 1 start, 2 chunk 0 done, 3 end, 4 waited
+  int32_t* prof_scratch;   // mask kernel, int32 profiles in HBM: kdim x 64 x R ints per (pair, wave)
 };
 
 struct BgFinishArgs {

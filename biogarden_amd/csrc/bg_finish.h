@@ -18,8 +18,8 @@
 #ifndef BG_FIN_DEBUG
 #define BG_FIN_DEBUG 0     // range checks with printf in the traceback (diagnosis builds)
 #endif
-#ifndef BG_NO_SEQCHECK
-#define BG_NO_SEQCHECK 0   // experiment: skip the walker's post-decode slot check
+#ifndef BG_SEQCHECK
+#define BG_SEQCHECK 0      // verification builds: the walker re-checks its decode (reanchor)
 #endif
 #ifndef BG_FIN_WAKEUP
 #define BG_FIN_WAKEUP 0
@@ -410,8 +410,12 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
 #pragma unroll
   for (int z = 0; z < kCkSlots; ++z) { ckS[z] = -1; ckC[z] = -1; }
   // decodes the 8x8 neighbourhood anchored at (k, l): lane (dk, dl) holds cell (k - dk, l - dl)
-  // 4-bit code of cell (kk, ll) from the resident trace (window or recomputed chunks)
+  // 4-bit code of cell (kk, ll) from the resident trace (window or recomputed chunks); the chunk-
+  // map entry it used goes to usedIdx / usedE (verification builds, BG_SEQCHECK)
+  int usedIdx = -1;
+  unsigned usedE = 0;
   auto decode_cell = [&](int kk, int ll) -> int {
+    usedIdx = -1;
     if (kk <= 0 || ll <= 0) return kCodeBorder | ((kk == 0) ? 2 : 1);  // column 0 'X', row 0 'Y'
     const int vr = kk - 1;
     const int sidx = vr / ROWS, rem = vr - sidx * ROWS, r = rem / R, q = rem - r * R;
@@ -424,6 +428,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       if ((e >> 4) != (((unsigned)sidx << 16) | (unsigned)cc) || e == 0xFFFFFFFFu) return kCodeMiss;
       const int z = (int)(e & 15);
       if (z >= nSlots) return kCodeMiss;                 // never published (guard)
+      usedIdx = mi;
+      usedE = e;
       if constexpr (ACK) {
         // bit planes (aff_recomp): not-Y, not-X, x_trace 'I', y_trace 'I' [, local stop]
         constexpr int NP = ack_planes<MODE == BGK_LOCAL>();
@@ -468,19 +474,25 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       __hip_atomic_store(&sh[35], la, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     const u64 td0 = F.dbg ? __builtin_readcyclecounter() : 0;
-    if (CK && asyncPos && !BG_NO_SEQCHECK) {
-      // Asynchronous recomputation: a helper may re-assign a slot while this decode reads it (it
-      // judged the walker's footprint from the position posted before this one, or the slot's
-      // map entry had been replaced by a colliding chunk).  Helpers bump the eviction epoch
-      // sh[59] when they claim a slot that held a chunk, before they write into it, and one
-      // wave's LDS operations complete in order: an epoch unchanged across the decode proves no
-      // slot it read was re-assigned meanwhile; otherwise decode again.
+    if (CK && asyncPos && BG_SEQCHECK) {
+      // Verification builds (BG_SEQCHECK=1): prove that no slot this decode read was re-assigned
+      // meanwhile.  A helper invalidates a slot's map entry before it writes into the slot and
+      // one wave's LDS operations complete in order, so every lane re-reads the entry it used
+      // after the decode; a changed entry means the codes may be torn: decode again.  The
+      // shipped build relies on the eviction rules instead (see the helper loop): for prefetches
+      // a helper evicts only empty, dead (right of / below a position the walker has already
+      // left) or stale slots, and footprint-unguarded ones only for a pending request, while the
+      // walker waits and decodes nothing; a served request is withdrawn at once, so no helper
+      // acts on one the walker has moved past.  tools/verify_seqcheck.sh counts the retries.
       for (;;) {
-        const int e0 = __hip_atomic_load(&sh[59], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
         codes = decode_cell(k0 - (lane >> 3), l0 - (lane & 7));
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (__hip_atomic_load(&sh[59], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == e0) break;
+        const bool same = usedIdx < 0 ||
+            __hip_atomic_load(&ckMap[usedIdx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == usedE;
+        if (!ballot(!same)) break;
+#if BG_FIN_DEBUG
+        if (lane == 0) printf("BGDBG pair %d: a slot was re-assigned during the decode at (%d, %d)\n", P.index, k0, l0);
+#endif
       }
     } else {
       codes = decode_cell(k0 - (lane >> 3), l0 - (lane & 7));
@@ -531,7 +543,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   asyncPos = async;
   if (async) {
     if (tid == 0) {
-      sh[32] = 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0; sh[37] = 0; sh[56] = -1; sh[59] = 0;
+      sh[32] = 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0; sh[37] = 0; sh[56] = -1;
       for (int z = 0; z < 8; ++z) { sh[40 + z] = -1; sh[48 + z] = 0; }
     }
     __syncthreads();
@@ -601,8 +613,6 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           if (oz >= 0) {
             unsigned& oe = ckMap[ck_map_idx(oz >> 16, oz & 0xffff)];
             if (oe == enc(oz, pick)) __hip_atomic_store(&oe, 0xFFFFFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            // the walker's decode check (reanchor): this slot is about to be overwritten
-            __hip_atomic_store(&sh[59], sh[59] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
           sh[40 + pick] = kk;
           sh[48 + pick] = 1;

@@ -28,7 +28,8 @@
 
 extern "C" void* bg_dp_kernel_ptr(int R, int affine, int local, int dna);
 extern "C" int bg_dp_has_R(int R, int affine, int local, int dna);
-extern "C" void* bg_dp_kernel_p32_ptr(int R, int affine, int local);
+extern "C" void* bg_dp_kernel_p32_ptr(int R, int affine, int local, int global);
+extern "C" void* bg_dp_kernel_lcs_ptr(int R, int dna);
 extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt);
 extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode);
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
@@ -167,6 +168,7 @@ struct bg_aligner {
   int allowAck = 1;
   int ckpt = 0;                    // tagged path: score-only DP + checkpoint traceback
   int p32 = 0;                     // mask kernel with int32 profile entries (S - a beyond int16)
+  int pglob = 0;                   // ... with the per-wave profile tables in HBM (too big for LDS)
   int pstride = 32;                // int16 profile table row stride (the batch's dense alphabet, >= 32)
   std::vector<uint64_t> pmaskW;    // prepare: 256-bit code sets per pair (alphabets beyond 32)
   int finFlags = 0;                // BG_FIN_* for the finish kernel (edit distance, LCS)
@@ -183,7 +185,7 @@ struct bg_aligner {
   std::vector<int2> wgmap;
   int gridWgs = 0;
   uint32_t progWords = 0;
-  DevBuf wgmapBuf, gprogBuf, dbgBuf, dpDbg;
+  DevBuf wgmapBuf, gprogBuf, dbgBuf, dpDbg, profScratch;
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
   float dp_ms = 0.f, fin_ms = 0.f;
@@ -207,7 +209,8 @@ struct bg_aligner {
   uint64_t nPrepare = 0, nFetch = 0;
 
   size_t device_bytes() const {
-    size_t t = seq1.cap + seq2.cap + codes1.cap + codes2.cap + lut.cap + prof.cap + pairs.cap + recs.cap;
+    size_t t = seq1.cap + seq2.cap + codes1.cap + codes2.cap + lut.cap + prof.cap + pairs.cap + recs.cap +
+               profScratch.cap;
     for (const Slot& S : slot)
       t += S.trace.cap + S.bndM.cap + S.bndX.cap + S.aux.cap + S.out1.cap + S.out2.cap + S.results.cap;
     return t;
@@ -290,7 +293,7 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   if (h->stream3) (void)hipStreamSynchronize(h->stream3);
   for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs,
-                    &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg}) d->release();
+                    &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg, &h->profScratch}) d->release();
   for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
   for (Slot& S : h->slot) {
     for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results}) d->release();
@@ -437,7 +440,8 @@ static int vgprs_of(const void* fn) {
 static void* dp_fn(const bg_aligner* h, int R) {
   if (h->tag) return bg_dp_kernel_tag_ptr(R, 0, h->ckpt);
   if (h->ack) return bg_dp_aff_kernel_ptr(R, h->local);
-  if (h->p32) return bg_dp_kernel_p32_ptr(R, h->affine, h->local);
+  if (h->p32) return bg_dp_kernel_p32_ptr(R, h->affine, h->local, h->pglob);
+  if (h->finFlags & BG_FIN_LCS) return bg_dp_kernel_lcs_ptr(R, h->dna);
   return bg_dp_kernel_ptr(R, h->affine, h->local, h->dna);
 }
 static void* fin_fn(const bg_aligner* h, int R) {
@@ -554,7 +558,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
       if (!h->tag && !h->ack && !h->dna) {
         // mask kernel, LDS profiles: lut, the 32 x 32 table, then per wave K x 64 lanes x WPE
         const size_t wpe = h->p32 ? (size_t)Rc : (size_t)(Rc + 1) / 2;
-        if (256 + (h->p32 ? 4096 : 2048) + (size_t)h->kdim * 64 * wpe * 4 + 64 > 160 * 1024) continue;
+        if (!h->pglob && 256 + (h->p32 ? 4096 : 2048) + (size_t)h->kdim * 64 * wpe * 4 + 64 > 160 * 1024) continue;
       }
       if (h->ack) {
         const size_t ldsCu = 160 * 1024 > finLdsRes ? 160 * 1024 - finLdsRes : 0;
@@ -724,6 +728,8 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   // S - a beyond int16 (the reference's closure is any i32): the mask kernel with int32 profile
   // entries (bg_dp_kernel<4, ..., P32>), which keeps the reference's wrapping i32 arithmetic
   h->p32 = (!dnaOK && !i16OK) ? 1 : 0;
+  // one wave's K x 64 x R int32 profile (R = 4) beyond the CU's LDS: the tables go to HBM
+  h->pglob = (h->p32 && 256 + 4096 + (size_t)std::max(K, 1) * 64 * 4 * 4 + 64 > 160 * 1024) ? 1 : 0;
   h->dna = dnaOK ? 1 : 0;
   h->kdim = std::max(K, 1);
   h->pstride = std::max(K, 32);         // row stride of the int16 profile table in HBM
@@ -809,16 +815,16 @@ plan_again:
     }
   } else {
     lds = 256;               // lut (+ int16 / int32 table and per-wave profiles on the LDS path)
-    if (!h->dna) {
+    if (h->pglob) {
+      lds = 256 + 4096;      // lut + the 32 x 32 int32 table slot; the profiles live in HBM
+    } else if (!h->dna) {
       const int WPE = h->p32 ? R : (R + 1) / 2;
       for (;;) {
         lds = 256 + (h->p32 ? 4096 : 2048) + (size_t)W * h->kdim * 64 * WPE * 4;
         if (lds + 64 <= 160 * 1024 || W == 1) break;
         --W;
       }
-      // one wave's K x 64 int32 profile beyond the CU's LDS: more than ~150 symbols with scores
-      // beyond int16 (the only case left without a kernel)
-      if (lds + 64 > 160 * 1024) return BG_E_ALPHABET;
+      if (lds + 64 > 160 * 1024) return BG_E_ALPHABET;   // unreachable: pglob covers it
     }
     h->progOff = (int)lds;   // 16 per-wave progress counters follow
     lds += 64;
@@ -908,7 +914,8 @@ plan_again:
       !h->codes2.ensure(o2 + 16) || !h->lut.ensure(256) ||
       !h->prof.ensure(std::max<size_t>(4096, (size_t)h->pstride * h->pstride * 4 + 64)) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
       !h->wgmapBuf.ensure(sizeof(int2) * (h->wgmap.size() + 1)) ||
-      !h->gprogBuf.ensure(4 * ((size_t)h->progWords + 1)))
+      !h->gprogBuf.ensure(4 * ((size_t)h->progWords + 1)) ||
+      (h->pglob && !h->profScratch.ensure((h->plan.size() + 1) * (size_t)h->W * h->kdim * 64 * 4 * 4)))
     return BG_E_NOMEM;
   h->gridWgs = h->wide ? (int)h->wgmap.size() : (int)h->plan.size();
   for (int z = 0; z < h->depth; ++z) {
@@ -1084,6 +1091,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, h->stream));
     }
     if (h->wide) BG_HIP(hipMemsetAsync(h->gprogBuf.p, 0, 4 * (size_t)h->progWords, h->stream));
+    A.prof_scratch = h->pglob ? h->profScratch.as<int32_t>() : nullptr;
     A.trace = S.trace.as<uint32_t>();
     A.bndM = S.bndM.as<int32_t>();
     A.bndX = S.bndX.as<int32_t>();
@@ -1520,7 +1528,8 @@ extern "C" int bg_lcs_batch(bg_aligner* h, size_t npairs, const uint8_t* const* 
   h->allowAck = 1;
   h->finFlags = BG_FIN_LCS;
   rc = prepare_impl(h, BG_GLOBAL, npairs, s1, n1, s2, n2, sc, 0, 0);
-  if (!rc && !h->ack) rc = BG_E_SCORE_RANGE;          // sizes beyond the frame's range
+  // (pairs beyond the checkpoint tracebacks' chunk keys run the full-trace mask kernel with the
+  // LCS rule in its trace bits, bg_dp_kernel<4, ..., LCS>)
   if (!rc) rc = bg_batch_execute(h);
   std::vector<bg_pair_result> res(npairs);
   std::vector<uint8_t> a1(h->outBytes + 1), ops(h->outBytes + 1);

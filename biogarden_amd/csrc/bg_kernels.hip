@@ -72,7 +72,11 @@ enum { VAR_FAST = 0, VAR_SEL = 1, VAR_EDGE = 2 };
 template <int R, bool P32>
 struct MaskWPE { static constexpr int v = P32 ? R : (R + 1) / 2; };
 
-template <int R, bool AFFINE, bool LOCAL, bool DNA, int VAR, bool P32 = false>
+// LCS (processing::patterns::longest_common_subsequence, patterns.rs:82-118; global mode, byte
+// equality +1 / -1, open = extend = 0): a match always moves diagonally, so its cell's trace bits
+// are cleared (a mismatch's diagonal is always strictly below up / left, and left-on-ties is the
+// aligner's Y > X priority already).
+template <int R, bool AFFINE, bool LOCAL, bool DNA, int VAR, bool P32 = false, bool LCS = false>
 __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx& C, int c, int bM,
                                           int bX, int cv) {
   const int a = C.a;
@@ -139,6 +143,11 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
       const int best = imax3(d, X, Yv);
       u64 mY = ballot(best == Yv);            // priority Y > X > R (aligner.rs:455-463)
       u64 mX = ballot(best == X) & ~mY;
+      if constexpr (LCS) {
+        const u64 match = ballot(sp > 0);
+        mY &= ~match;
+        mX &= ~match;
+      }
       if constexpr (LOCAL) {
         const u64 z = ballot(best == 0);      // M == 0: backtrack stops here (:181)
         mY |= z;
@@ -224,7 +233,11 @@ __device__ __forceinline__ void run_chunk(Strip<R, AFFINE, LOCAL>& S, const Ctx&
 
 }  // namespace
 
-template <int R, bool AFFINE, bool LOCAL, bool DNA, bool P32 = false>
+// PGLOB (with P32): the per-wave int32 profile tables live in HBM (A.prof_scratch, one
+// kdim x 64 x R table per (pair, wave)) instead of LDS — alphabets whose table does not fit the
+// CU's LDS (more than ~150 codes with scores beyond int16); the step reads its entry through the
+// vector L1.  LCS: see run_chunk.
+template <int R, bool AFFINE, bool LOCAL, bool DNA, bool P32 = false, bool PGLOB = false, bool LCS = false>
 __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(BgDpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* sLut = smem;                                        // 256 B
@@ -271,7 +284,10 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
   const size_t stripDw = (size_t)NC * (BG_CHUNK / BG_TRACE_BLK) * R * NW * BG_WAVE;
 
   int* ldsProf = nullptr;
-  if constexpr (!DNA) ldsProf = reinterpret_cast<int*>(smem + 256 + TABB) + (size_t)w * A.kdim * BG_WAVE * MaskWPE<R, P32>::v;
+  if constexpr (PGLOB)
+    ldsProf = A.prof_scratch + ((size_t)blockIdx.x * W + w) * A.kdim * BG_WAVE * MaskWPE<R, P32>::v;
+  else if constexpr (!DNA)
+    ldsProf = reinterpret_cast<int*>(smem + 256 + TABB) + (size_t)w * A.kdim * BG_WAVE * MaskWPE<R, P32>::v;
 
   Ctx C;
   C.a = a; C.b = b; C.mode = mode;
@@ -375,9 +391,9 @@ __global__ __launch_bounds__((AFFINE || LOCAL) ? 512 : 1024) void bg_dp_kernel(B
         if constexpr (AFFINE) bX = load_agent(A.bndX + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
       }
       const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
-      if (edge) run_chunk<R, AFFINE, LOCAL, DNA, VAR_EDGE, P32>(S, C, c, bM, bX, cv);
-      else if (lastStrip && selRow) run_chunk<R, AFFINE, LOCAL, DNA, VAR_SEL, P32>(S, C, c, bM, bX, cv);
-      else run_chunk<R, AFFINE, LOCAL, DNA, VAR_FAST, P32>(S, C, c, bM, bX, cv);
+      if (edge) run_chunk<R, AFFINE, LOCAL, DNA, VAR_EDGE, P32, LCS>(S, C, c, bM, bX, cv);
+      else if (lastStrip && selRow) run_chunk<R, AFFINE, LOCAL, DNA, VAR_SEL, P32, LCS>(S, C, c, bM, bX, cv);
+      else run_chunk<R, AFFINE, LOCAL, DNA, VAR_FAST, P32, LCS>(S, C, c, bM, bX, cv);
       // publish: the chunk ends with the R trace stores of its second half; everything issued
       // before them (this chunk's boundary-row stores included) has reached L2 at vmcnt(R)
       asm volatile("s_waitcnt vmcnt(%0)" ::"i"(R) : "memory");
@@ -512,10 +528,28 @@ template __global__ void bg_dp_kernel<4, false, true, false, true>(BgDpArgs);
 template __global__ void bg_dp_kernel<4, true, false, false, true>(BgDpArgs);
 template __global__ void bg_dp_kernel<4, true, true, false, true>(BgDpArgs);
 
-extern "C" void* bg_dp_kernel_p32_ptr(int R, int affine, int local) {
+// ... with the per-wave profile tables in HBM (more than ~150 codes)
+template __global__ void bg_dp_kernel<4, false, false, false, true, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<4, false, true, false, true, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<4, true, false, false, true, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<4, true, true, false, true, true>(BgDpArgs);
+// LCS tie rule (bg_lcs_batch beyond the checkpoint tracebacks' chunk keys): linear global, R = 4
+template __global__ void bg_dp_kernel<4, false, false, true, false, false, true>(BgDpArgs);
+template __global__ void bg_dp_kernel<4, false, false, false, false, false, true>(BgDpArgs);
+
+extern "C" void* bg_dp_kernel_p32_ptr(int R, int affine, int local, int global) {
   if (R != 4) return nullptr;
+  if (global) {
+    if (affine) return local ? (void*)&bg_dp_kernel<4, true, true, false, true, true> : (void*)&bg_dp_kernel<4, true, false, false, true, true>;
+    return local ? (void*)&bg_dp_kernel<4, false, true, false, true, true> : (void*)&bg_dp_kernel<4, false, false, false, true, true>;
+  }
   if (affine) return local ? (void*)&bg_dp_kernel<4, true, true, false, true> : (void*)&bg_dp_kernel<4, true, false, false, true>;
   return local ? (void*)&bg_dp_kernel<4, false, true, false, true> : (void*)&bg_dp_kernel<4, false, false, false, true>;
+}
+extern "C" void* bg_dp_kernel_lcs_ptr(int R, int dna) {
+  if (R != 4) return nullptr;
+  return dna ? (void*)&bg_dp_kernel<4, false, false, true, false, false, true>
+             : (void*)&bg_dp_kernel<4, false, false, false, false, false, true>;
 }
 // metric-path (linear gaps, DNA register profile) kernels at extra strip heights: the planner
 // picks R so that a pair's strip count fills the workgroup's waves (DESIGN.md "Geometry")

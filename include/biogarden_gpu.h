@@ -58,9 +58,9 @@ enum {
   BG_E_ARG = -1,        /* bad argument (null pointer, capacity too small, unknown mode) */
   BG_E_HIP = -2,        /* HIP runtime failure */
   BG_E_NOMEM = -3,      /* device or host allocation failed */
-  BG_E_SCORE_RANGE = -4,/* LCS only: lengths beyond its value frame (scores beyond int16 run the int32-profile kernel) */
+  BG_E_SCORE_RANGE = -4,/* no longer returned (kept for ABI stability; LCS beyond the checkpoint keys runs the mask kernel) */
   BG_E_NO_BATCH = -5,   /* bg_batch_execute/fetch without a prepared batch */
-  BG_E_ALPHABET = -6,   /* more than ~150 symbols in a batch whose scores leave int16 */
+  BG_E_ALPHABET = -6,   /* no longer returned (kept for ABI stability; big int32 alphabets keep their profiles in HBM) */
   BG_E_IO = -7,         /* bg_fasta_open: the file cannot be opened */
   BG_E_FORMAT = -8,     /* bg_fasta_next_batch: "Expected > at record start." (fasta.rs:104-109) */
   BG_E_UTF8 = -9        /* bg_fasta_next_batch: a line is not valid UTF-8 (BufRead::read_line's
@@ -126,8 +126,8 @@ int bg_batch_prepare(bg_aligner* h, int mode, size_t npairs, const uint8_t* cons
  * code), code[byte] >= k marks a byte the closure panics on (status BG_UNSCORABLE).  Batches
  * using more than 32 codes run on the score-only affine-family kernels when their values fit
  * int8 (scores minus the open and extend penalties), otherwise on the mask-trace kernel reading
- * its k x k table from HBM; BG_E_ALPHABET only when one wave's k x 64 int32 profile exceeds the
- * CU's LDS (more than ~150 codes with scores beyond int16). */
+ * its k x k table from HBM (with the per-wave k x 64 int32 profiles in HBM too when they exceed
+ * the CU's LDS: more than ~150 codes with scores beyond int16). */
 int bg_batch_prepare_table(bg_aligner* h, int mode, size_t npairs, const uint8_t* const* s1,
                            const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                            const uint16_t* code, int32_t k, const int32_t* table, int32_t a,

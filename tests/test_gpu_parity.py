@@ -133,11 +133,16 @@ def test_custom_closure_beyond_int16(aligner, oracle, mode, a, b):
 
 @pytest.mark.parametrize("mode,a,b,nsym,big", [("global", -11, -1, 70, 900), ("local", -300, -300, 70, 900),
                                                 ("semiglobal", -5, -9, 200, 900), ("fitting", -40, -3, 256, 900),
-                                                ("overlap", -4, -6, 90, 40000), ("global", -30000, -2, 120, 40000)])
+                                                ("overlap", -4, -6, 90, 40000), ("global", -30000, -2, 120, 40000),
+                                                # K x 64 int32 profiles beyond the LDS: tables in HBM
+                                                ("global", -11, -1, 256, 40000), ("local", -300, -300, 200, 40000),
+                                                ("semiglobal", -5, -9, 160, 40000)])
 def test_wide_alphabet_beyond_int8(aligner, oracle, mode, a, b, nsym, big):
     """More than 32 symbols with scores the score-only int8 kernels cannot take (the reference's
     closure is any i32 over any bytes, score.rs:38-41): the mask-trace kernel, its k x k table
-    read from HBM (int16 entries, or int32 when S - a leaves int16), bit-exact with the oracle."""
+    read from HBM (int16 entries, or int32 when S - a leaves int16; beyond ~150 int32 codes the
+    per-wave profiles live in HBM too, where BG_E_ALPHABET used to refuse), bit-exact with the
+    oracle."""
     rng = random.Random(nsym * 7 + big - a)
     alpha = bytes(range(256 - nsym, 256))
 
