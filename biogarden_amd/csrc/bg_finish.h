@@ -489,9 +489,22 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         const bool same = usedIdx < 0 ||
             __hip_atomic_load(&ckMap[usedIdx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == usedE;
-        if (!ballot(!same)) break;
+        const u64 bad = ballot(!same);
+        if (!bad) break;
 #if BG_FIN_DEBUG
-        if (lane == 0) printf("BGDBG pair %d: a slot was re-assigned during the decode at (%d, %d)\n", P.index, k0, l0);
+        {
+          const int bl = (int)__builtin_ctzll(bad);
+          const unsigned ue = (unsigned)__shfl((int)usedE, bl, 64);
+          const int ui = __shfl(usedIdx, bl, 64);
+          const unsigned now = ckMap[ui];
+          const int vw = k0 - 1, sw = vw / ROWS, remw = vw - sw * ROWS, ccw = (l0 + remw / R) >> 6;
+          if (lane == 0)
+            printf("BGDBG pair %d: a slot was re-assigned during the decode at (%d, %d) strip %d chunk %d: "
+                   "lane %d read chunk (%u, %u) slot %u, entry now %08x, slots [%d %d %d %d %d %d %d %d] filling [%d%d%d%d%d%d%d%d] req %d\n",
+                   P.index, k0, l0, sw, ccw, bl, ue >> 20, (ue >> 4) & 0xffff, ue & 15, now,
+                   sh[40], sh[41], sh[42], sh[43], sh[44], sh[45], sh[46], sh[47],
+                   sh[48], sh[49], sh[50], sh[51], sh[52], sh[53], sh[54], sh[55], sh[33]);
+        }
 #endif
       }
     } else {
@@ -593,10 +606,16 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         };
         for (int q = 0; q < NCAND && key < 0; ++q) {
           const int kk = cand[q];
-          if (kk < 0 || resident(kk)) continue;
+          if (kk < 0) continue;
+          // a filler publishes the chunk in the map, then clears its slot's filling flag: read
+          // the flags first and the map second (acquire), or a chunk published between the two
+          // reads looks neither resident nor in flight and is recomputed into a second slot (its
+          // first copy then turns stale and may be evicted while the walker decodes from it)
           bool flying = false;
-          for (int z = 0; z < nSlots; ++z) flying |= (sh[48 + z] != 0 && sh[40 + z] == kk);
-          if (flying) continue;
+          for (int z = 0; z < nSlots; ++z)
+            flying |= (__hip_atomic_load(&sh[48 + z], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 &&
+                       sh[40 + z] == kk);
+          if (flying || resident(kk)) continue;
           // a slot: empty, stale (its chunk no longer in the map), dead, or (request) unguarded
           int pick = -1;
           for (int z = 0; z < nSlots && pick < 0; ++z) {
@@ -847,9 +866,14 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                 if (lane == 0) {
                   while (__hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
                     __builtin_amdgcn_s_sleep(1);
+                  // in flight (flags first), then published meanwhile (the map second): see the
+                  // helpers' candidate check
+                  bool busy = false;
+                  for (int z = 0; z < nSlots; ++z)
+                    busy |= (__hip_atomic_load(&sh[48 + z], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 &&
+                             sh[40 + z] == key);
                   const unsigned e2 = __hip_atomic_load(me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                  bool busy = e2 != 0xFFFFFFFFu && (int)(e2 >> 4) == key;     // published meanwhile
-                  for (int z = 0; z < nSlots; ++z) busy |= (sh[48 + z] != 0 && sh[40 + z] == key);
+                  busy |= e2 != 0xFFFFFFFFu && (int)(e2 >> 4) == key;
                   if (!busy) {
                     // the helpers' eviction order: an empty, stale or dead slot first (dead =
                     // right of / below the walker, never read again), then one outside the
