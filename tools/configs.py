@@ -93,7 +93,9 @@ def main():
         dp, fin, n = h.profile_end()
         res = h.fetch()
         bad = sum(1 for r in res if r["status"] not in (0, 4))
+        bpc = 0.25 if a >= b else 0.5          # SURVEY §8(d) algorithmic bytes per cell
         line = {"config": name, "mode": mode, "pairs": len(pairs), "cells": st["cells"],
+                "algorithmic_bytes": int(st["cells"] * bpc + st["residue_bytes"]),
                 "gcups": round(st["cells"] / el / 1e9, 2), "ms_per_step": round(el * 1e3, 3),
                 "dp_ms": round(dp, 3), "finish_ms": round(fin, 3), "prepare_s": round(prep, 3),
                 "R": st["R"], "waves": st["waves"], "affine": st["affine"], "tagged": st["tagged"],
