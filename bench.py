@@ -200,18 +200,25 @@ def timed(h, steps, warmup, barrier, per_step=None):
     return elapsed, dp_ms, fin_ms
 
 
-def gatherer(h, dist, coll_dev):
-    """Per-step §8(e) result path: bg_batch_export packs the last execute's records and strings
-    device-to-device, then one variable-size gather to rank 0 (RCCL over xGMI; gloo rehearsal on
-    host tensors).  Returns a callable -> rank 0: list of per-rank packed bytes."""
+def gatherer(h, dist, coll_dev, stats=None):
+    """Per-step §8(e) result path: bg_batch_export_compact packs the last execute's headers and
+    alignment cores (2-bit edit scripts) device-to-device, then one variable-size gather to rank 0
+    (RCCL send/recv over xGMI; gloo rehearsal on host tensors).  Returns a callable -> rank 0:
+    list of per-rank records (bytes); `stats` (dict) receives the payload bytes."""
     import torch
     from biogarden_amd import shard
-    nbytes = h.export_size()
-    local = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda")
+    buf = {"t": None}
 
     def step():
-        h.export_to(local.data_ptr(), nbytes)
-        src = local[:nbytes]
+        n = h.export_compact_size()
+        if buf["t"] is None or buf["t"].numel() < n:
+            buf["t"] = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
+        h.export_compact_to(buf["t"].data_ptr(), n)
+        src = buf["t"][:n]
+        if stats is not None:
+            stats["record_bytes"] = n
+        if dist is None:
+            return [src.cpu().numpy().tobytes()]
         return shard.gather_packed(src if coll_dev == "cuda" else src.cpu(), dist, dst=0)
     return step
 
@@ -438,21 +445,19 @@ def main():
     # ---- results: RCCL gather of every rank's packed results to rank 0 (after the timed
     # region for the weak form; the strong form gathered inside every step)
     gather_ms = None
-    results0 = None
+    heads0 = None
+    gstats = {}
     if dist is not None and not args.no_gather:
-        g = gstep or gatherer(h, dist, coll_dev)
+        g = gstep or gatherer(h, dist, coll_dev, gstats)
         barrier()
         tg = time.perf_counter()
         packed = g()
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         if rank == 0:
-            results0 = [_native.decode_export(b) for b in packed]
+            heads0 = [_native.compact_headers(b) for b in packed]
     else:
-        nbytes = h.export_size()
-        local = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda")
-        h.export_to(local.data_ptr(), nbytes)
-        results0 = [_native.decode_export(local[:nbytes].cpu().numpy().tobytes())]
+        heads0 = [_native.compact_headers(b) for b in gatherer(h, None, coll_dev, gstats)()]
     workload = workload_name(args.mode, args.pairs, args.len1, args.len2, args.open, args.extend)
     roof = roofline(st, cells, dp_ms, workload, args.open, args.extend)
     roof["finish_ms"] = round(fin_ms, 4)
@@ -514,8 +519,8 @@ def main():
             dist.destroy_process_group()
         return
 
-    ok_status = all(r["status"] == 0 for rr in results0 for r in rr)
-    gpu_scores = [r["score"] for r in results0[0]]
+    ok_status = all(st == 0 for rr in heads0 for st, _, _ in rr)
+    gpu_scores = [sc for _, sc, _ in heads0[0]]
 
     # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0, N = 1)
     cpu = None
@@ -550,6 +555,7 @@ def main():
         "strong": strong,
         "configs": cfgs,
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
+        "gather_record_bytes_per_rank": gstats.get("record_bytes"),
         "host_to_host": h2h,
         "all_status_ok": ok_status,
     }
@@ -570,7 +576,8 @@ def job_line(args, h, sc, world, rank, dist, coll_dev, barrier, max_over_ranks, 
     h.set_call_dims(dims)
     h.prepare(mode, pairs, sc, a, b)
     st = h.stats()
-    g = gatherer(h, dist, coll_dev) if dist is not None else None
+    gstats = {}
+    g = gatherer(h, dist, coll_dev, gstats)
     steps = args.steps
     el, dp, fin = timed(h, steps, args.warmup, barrier, g)
     el = max_over_ranks(el)
@@ -578,18 +585,16 @@ def job_line(args, h, sc, world, rank, dist, coll_dev, barrier, max_over_ranks, 
     # the same job without the per-step gather (executes pipelined back to back)
     el2, _, _ = timed(h, steps, 1, barrier)
     el2 = max_over_ranks(el2)
-    if g is not None:
-        packed = g()
-    else:
-        nbytes = h.export_size()
-        local = torch.empty(max(nbytes, 1), dtype=torch.uint8, device="cuda")
-        h.export_to(local.data_ptr(), nbytes)
-        packed = [local[:nbytes].cpu().numpy().tobytes()]
+    packed = g()
     roof = roofline(st, st["cells"], dp, name, a, b)
     roof["finish_ms"] = round(fin, 4)
     if rank == 0:
         from biogarden_amd import shard
-        merged = shard.merge_shards(shards, [_native.decode_export(x) for x in packed])
+        # rank 0 expands every rank's edit scripts into the aligned strings (it holds the inputs)
+        te = time.perf_counter()
+        per = [_native.expand_compact(rec, [allp[p] for p in idx]) for rec, idx in zip(packed, shards)]
+        expand_ms = (time.perf_counter() - te) * 1e3
+        merged = shard.merge_shards(shards, per)
         line = {"metric": "GCUPS (billion DP cells/s), %s, %d MI355X" % (name, world),
                 "value": round(total * steps / el / 1e9, 3), "unit": "GCUPS", "n_gpus": world,
                 "steps": steps, "warmup": args.warmup, "ms_per_step": round(el / steps * 1e3, 4),
@@ -601,6 +606,10 @@ def job_line(args, h, sc, world, rank, dist, coll_dev, barrier, max_over_ranks, 
                                           "gather to rank 0 in every step)" % world},
                 "pipelined_no_gather": {"value": round(total * steps / el2 / 1e9, 3),
                                         "ms_per_step": round(el2 / steps * 1e3, 4)},
+                "gather_record_bytes_rank0": gstats.get("record_bytes"),
+                "expand_ms": round(expand_ms, 2),
+                "expand_covers": "rank 0, bg_compact_expand of every rank's record into aligned "
+                                 "strings (host, after the timed steps)",
                 "roofline": roof,
                 "all_status_ok": all(r is not None and r["status"] in (0, 4) for r in merged)}
         print(json.dumps(line))

@@ -22,7 +22,8 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_abi_version", "bg_profile_begin", "bg_profile_end", "bg_batch_export",
            "bg_set_pipeline", "bg_set_kernel_options", "bg_edit_distance_batch",
            "bg_lcs_batch", "bg_aligner_buffer_size", "bg_aligner_set_buffer_size",
-           "bg_aligner_set_call_dims", "bg_host_timing", "bg_last_hip_error", "bg_fasta_open",
+           "bg_aligner_set_call_dims", "bg_host_timing", "bg_last_hip_error",
+           "bg_batch_export_compact", "bg_compact_expand", "bg_fasta_open",
            "bg_batch_prepare_table", "bg_fasta_next_batch",
            "bg_fasta_close"]
 
@@ -128,6 +129,12 @@ def lib():
     L.bg_profile_begin.argtypes = [ctypes.c_void_p]
     L.bg_profile_end.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
+    L.bg_batch_export_compact.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.POINTER(ctypes.c_size_t)]
+    L.bg_compact_expand.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                    ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
+                                    ctypes.POINTER(BgPairResult), c_u8p, c_u8p, ctypes.c_size_t]
     L.bg_host_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
                                  ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.bg_batch_export.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
@@ -321,6 +328,18 @@ class Handle:
         check(lib().bg_batch_export(self._p, ctypes.c_void_p(device_ptr), ctypes.byref(n)))
         return n.value
 
+    def export_compact_size(self):
+        """Bytes of the compact export record of the last execute (computes it on the device)."""
+        n = ctypes.c_size_t(0)
+        check(lib().bg_batch_export_compact(self._p, None, ctypes.byref(n)))
+        return n.value
+
+    def export_compact_to(self, device_ptr, nbytes):
+        """Writes the compact record (bg_batch_export_compact) to device memory of this GPU."""
+        n = ctypes.c_size_t(nbytes)
+        check(lib().bg_batch_export_compact(self._p, ctypes.c_void_p(device_ptr), ctypes.byref(n)))
+        return n.value
+
     def edit_distance_batch(self, pairs):
         """analysis::seq::edit_distance over pairs [(s1, s2)] -> [int]."""
         a1, n1, a2, n2, _ = self._arrays(pairs)
@@ -375,6 +394,40 @@ class Handle:
         st = BgStats()
         check(lib().bg_get_stats(self._p, ctypes.byref(st)))
         return {f: getattr(st, f) for f, _ in BgStats._fields_}
+
+
+def expand_compact(rec, pairs):
+    """bg_compact_expand: a compact export record (bytes) of `pairs` [(s1, s2)] -> the result
+    dicts bg_batch_fetch gives for them (status, score, both aligned strings, end, start)."""
+    rec = bytes(rec)
+    a1, n1, a2, n2, total = Handle._arrays(pairs)
+    n = len(pairs)
+    res = (BgPairResult * max(n, 1))()
+    o1 = (ctypes.c_uint8 * max(total, 1))()
+    o2 = (ctypes.c_uint8 * max(total, 1))()
+    check(lib().bg_compact_expand(rec, len(rec), n, a1, n1, a2, n2, res, o1, o2, total))
+    b1, b2 = bytes(o1), bytes(o2)
+    out = []
+    for p in range(n):
+        r = res[p]
+        lo, hi = r.offset, r.offset + r.len
+        out.append({"status": r.status, "score": r.score, "aligned1": b1[lo:hi], "aligned2": b2[lo:hi],
+                    "end": (r.end_i, r.end_j), "start": (r.start1, r.start2)})
+    return out
+
+
+def compact_headers(rec):
+    """The per-pair (status, score, len) of a compact export record, without expanding strings."""
+    import struct
+    rec = bytes(rec)
+    magic, n, _ops, _mode = struct.unpack_from("<4Q", rec, 0)
+    if magic != 0x31434742:
+        raise ValueError("not a compact export record")
+    out = []
+    for p in range(n):
+        st, sc, _off, ln = struct.unpack_from("<iiQI", rec, 32 + 48 * p)
+        out.append((st, sc, ln))
+    return out
 
 
 def decode_export(buf):

@@ -33,6 +33,7 @@ struct BgPair {
   uint32_t prog_off;   // WIDE mode: offset of the pair's wg_count*W progress counters in gprog
   int32_t buf_rows;    // the reference aligner's scratch when this pair's call starts (rows, cols)
   int32_t buf_cols;
+  uint64_t ops_off;    // byte offset of this pair's packed core ops (ceil((n1+n2)/4) bytes)
 };
 
 // Would the reference SequenceAligner, whose scratch is rows x cols when this call starts
@@ -74,6 +75,8 @@ struct BgResult {
   uint32_t out_start;      // aligned strings occupy [out_start, n1+n2) of the pair's slot
   uint32_t out_len;
   uint32_t start1, start2; // cell (k, l) where the traceback walk stopped
+  uint32_t npre, ntail;    // semiglobal prefix / tail gap columns (aligner.rs:389-428); the core's
+                           // out_len - npre - ntail ops are packed 2 bits each at F.ops + ops_off
 };
 
 struct BgDpArgs {
@@ -136,6 +139,7 @@ struct BgFinishArgs {
   int32_t flags;           // BG_FIN_* below
   int32_t nslots;          // checkpoint modes: recomputed-chunk slots in use (0: all)
   int32_t pstride;         // row stride of the int16 profile table (affine checkpoint path)
+  uint8_t* ops;            // packed core ops (2 bits per column, op 0 diagonal, 1 up, 2 left)
 };
 
 // BgFinishArgs::flags
@@ -152,6 +156,26 @@ struct BgPairResultDev {
   int32_t status, score;
   uint64_t offset;
   uint32_t len, end_i, end_j, start1, start2, reserved;
+};
+
+// Compact export (bg_batch_export_compact): per caller pair a header, then the pairs' packed core
+// ops back to back.  The layout is include/biogarden_gpu.h's bg_compact_hdr.
+struct BgCompactHdr {
+  int32_t status, score;
+  uint64_t ops_off;        // byte offset of the packed ops in the record's ops area
+  uint32_t len, end_i, end_j, start1, start2, npre, ntail, reserved;
+};
+
+struct BgCompactArgs {
+  const BgPair* pairs;
+  const BgResult* results;
+  const BgPairResultDev* recs;   // caller-order template (pre-decided statuses)
+  const uint8_t* ops;            // the slot's packed ops (BgPair::ops_off)
+  uint64_t* sizes;               // caller order: packed bytes, then (scan) offsets; [n] = total
+  uint8_t* dst;                  // the record
+  uint64_t npairs_caller;
+  int32_t nplan;
+  int32_t mode;
 };
 
 struct BgExportArgs {

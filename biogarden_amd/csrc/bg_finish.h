@@ -1100,6 +1100,18 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   const int hi = lo + seg < cend ? lo + seg : cend;
   int c1 = 0, c2 = 0;
   for (int x = lo; x < hi; ++x) { const int op = ob[x]; c1 += op != 2; c2 += op != 1; }
+  // the core's ops, 2 bits per column (the compact export's payload, bg_batch_export_compact),
+  // before the expansion below overwrites them with residues
+  if (F.ops) {
+    uint8_t* po = F.ops + P.ops_off;
+    for (int g = tid; g < (ncore + 3) / 4; g += NT) {
+      unsigned v = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (4 * g + q < ncore) v |= (unsigned)(ob[cbase + 4 * g + q] & 3) << (2 * q);
+      po[g] = (uint8_t)v;
+    }
+  }
   scan[tid] = c1;
   scan[NT + tid] = c2;
   __syncthreads();
@@ -1148,6 +1160,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     res.out_len = (uint32_t)L;
     res.start1 = (uint32_t)kstop;
     res.start2 = (uint32_t)lstop;
+    res.npre = (uint32_t)npre;
+    res.ntail = (uint32_t)ntail;
     F.results[P.index] = res;
   }
 }

@@ -38,6 +38,9 @@ extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes(int win_bytes);
 extern "C" int bg_finish_window_bytes(int R, int affine, size_t npairs, int cus);
 extern "C" void* bg_export_kernel_ptr();
+extern "C" void* bg_compact_size_kernel_ptr();
+extern "C" void* bg_compact_scan_kernel_ptr();
+extern "C" void* bg_compact_write_kernel_ptr();
 extern "C" void* bg_code_kernel_ptr();
 extern "C" void* bg_global_score_kernel_ptr();
 extern "C" void* bg_dp_aff_kernel_ptr(int R, int local);
@@ -127,7 +130,7 @@ struct PhaseTimer {
 // Per-execute arenas.  Two slots let the finish kernel of execute k (stream2) run while the
 // DP kernel of execute k+1 (stream) fills the other slot's trace.
 struct Slot {
-  DevBuf trace, bndM, bndX, aux, out1, out2, results;
+  DevBuf trace, bndM, bndX, aux, out1, out2, results, ops;
   hipEvent_t dpDone = nullptr, finDone = nullptr;
   bool inflight = false;
 };
@@ -185,7 +188,10 @@ struct bg_aligner {
   std::vector<int2> wgmap;
   int gridWgs = 0;
   uint32_t progWords = 0;
-  DevBuf wgmapBuf, gprogBuf, dbgBuf, dpDbg, profScratch;
+  DevBuf wgmapBuf, gprogBuf, dbgBuf, dpDbg, profScratch, compactSizes;
+  int compactExec = -1;            // bg_batch_export_compact: the execute its sizes were made for
+  uint64_t compactOps = 0;
+  uint64_t opsBytes = 0;           // packed core ops per slot (sum of ceil((n1+n2)/4))
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
   float dp_ms = 0.f, fin_ms = 0.f;
@@ -212,7 +218,8 @@ struct bg_aligner {
     size_t t = seq1.cap + seq2.cap + codes1.cap + codes2.cap + lut.cap + prof.cap + pairs.cap + recs.cap +
                profScratch.cap;
     for (const Slot& S : slot)
-      t += S.trace.cap + S.bndM.cap + S.bndX.cap + S.aux.cap + S.out1.cap + S.out2.cap + S.results.cap;
+      t += S.trace.cap + S.bndM.cap + S.bndX.cap + S.aux.cap + S.out1.cap + S.out2.cap + S.results.cap +
+           S.ops.cap;
     return t;
   }
 };
@@ -293,10 +300,11 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   if (h->stream3) (void)hipStreamSynchronize(h->stream3);
   for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs,
-                    &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg, &h->profScratch}) d->release();
+                    &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg, &h->profScratch, &h->compactSizes})
+    d->release();
   for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
   for (Slot& S : h->slot) {
-    for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results}) d->release();
+    for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops}) d->release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
     if (S.finDone) (void)hipEventDestroy(S.finDone);
   }
@@ -851,7 +859,7 @@ plan_again:
   h->plan.reserve(order.size());
   h->wgmap.clear();
   h->progWords = 0;
-  uint64_t tro = 0, bo = 0, ao = 0, oo = 0;
+  uint64_t tro = 0, bo = 0, ao = 0, oo = 0, po = 0;
   h->cells = 0;
   for (size_t p : order) {
     BgPair P;
@@ -880,6 +888,8 @@ plan_again:
     ao += round_up((uint64_t)(n1[p] + 1) + (h->local ? 2 * n1[p] : 0), 64);
     P.out_off = oo;
     oo += n1[p] + n2[p];
+    P.ops_off = po;
+    po += (n1[p] + n2[p] + 3) / 4;
     P.wg_count = h->wide ? std::max(1, h->groupOf[p]) : 1;
     P.prog_off = h->wide ? h->progWords : 0;
     P.buf_rows = (int32_t)std::min<long>(h->bufAt[p].first, 0x7FFFFFFF);
@@ -905,6 +915,8 @@ plan_again:
     h->plan.push_back(P);
   }
   h->traceBytes = tro;
+  h->opsBytes = po;
+  h->compactExec = -1;
   h->bndBytes = bo * 4 * ((h->affine || h->ack) ? 2 : 1);
   h->resBytes = o1 + o2;
 
@@ -922,7 +934,7 @@ plan_again:
     Slot& S = h->slot[z];
     if (!S.trace.ensure(tro + 256) || !S.bndM.ensure(bo * 4 + 256) ||
         !S.bndX.ensure((h->affine || h->ack) ? bo * 4 + 256 : 256) || !S.aux.ensure(ao * 4 + 256) ||
-        !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) ||
+        !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) || !S.ops.ensure(po + 16) ||
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)))
       return BG_E_NOMEM;
   }
@@ -1146,6 +1158,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.bndX = S.bndX.as<int32_t>();
     F.kdim = h->kdim;
     F.pstride = h->pstride;
+    F.ops = S.ops.as<uint8_t>();
     F.area_ints = 0;
     F.flags = h->finFlags;
     if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;
@@ -1449,6 +1462,57 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   BG_HIP(hipStreamSynchronize(h->stream));
   *bytes = need;
   return BG_OK;
+}
+
+extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) {
+  if (!h || !bytes) return BG_E_ARG;
+  if (!h->prepared || !h->executed) return BG_E_NO_BATCH;
+  BG_HIP(hipSetDevice(h->device));
+  const uint64_t n = h->npairs;
+  const Slot& S = h->slot[h->lastSlot];
+  BgCompactArgs E;
+  E.pairs = h->pairs.as<BgPair>();
+  E.results = S.results.as<BgResult>();
+  E.recs = h->recs.as<BgPairResultDev>();
+  E.ops = S.ops.as<uint8_t>();
+  E.npairs_caller = n;
+  E.nplan = (int32_t)h->plan.size();
+  E.mode = h->mode;
+  void* args[] = {&E};
+  if (h->compactExec != h->execCount) {
+    // sizes and their scan for this execute (after its traceback), then the total to the host
+    if (!h->compactSizes.ensure(8 * (n + 1))) return BG_E_NOMEM;
+    E.sizes = h->compactSizes.as<uint64_t>();
+    E.dst = nullptr;
+    BG_HIP(hipStreamSynchronize(h->stream2));
+    BG_HIP(hipStreamSynchronize(h->stream3));
+    BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), h->stream));
+    const unsigned g = (unsigned)(((uint64_t)E.nplan + 255) / 256);
+    if (g) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(g), dim3(256), args, 0, h->stream));
+    BG_HIP(hipLaunchKernel(bg_compact_scan_kernel_ptr(), dim3(1), dim3(1024), args, 0, h->stream));
+    BG_HIP(hipMemcpyAsync(&h->compactOps, E.sizes + n, 8, hipMemcpyDeviceToHost, h->stream));
+    BG_HIP(hipStreamSynchronize(h->stream));
+    h->compactExec = h->execCount;
+  }
+  const size_t need = 32 + n * sizeof(bg_compact_hdr) + h->compactOps;
+  if (!dst) { *bytes = need; return BG_OK; }
+  if (*bytes < need) return BG_E_ARG;
+  E.sizes = h->compactSizes.as<uint64_t>();
+  E.dst = (uint8_t*)dst;
+  // plan pairs, then enough workgroups for the caller pairs decided on the host (and the head)
+  const unsigned g = (unsigned)E.nplan + (unsigned)((n + 255) / 256) + 1;
+  BG_HIP(hipLaunchKernel(bg_compact_write_kernel_ptr(), dim3(g), dim3(256), args, 0, h->stream));
+  BG_HIP(hipStreamSynchronize(h->stream));
+  *bytes = need;
+  return BG_OK;
+}
+
+extern "C" int bg_compact_expand(const void* rec, size_t rec_bytes, size_t npairs,
+                                 const uint8_t* const* s1, const size_t* n1, const uint8_t* const* s2,
+                                 const size_t* n2, bg_pair_result* results, uint8_t* out1,
+                                 uint8_t* out2, size_t out_cap) {
+  return bgh::compact_expand(static_cast<const uint8_t*>(rec), rec_bytes, npairs, s1, n1, s2, n2,
+                             results, out1, out2, out_cap);
 }
 
 // ------------------------------------------------------------------ edit distance, LCS

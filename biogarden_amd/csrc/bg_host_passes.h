@@ -290,4 +290,73 @@ inline void unpack_strings(const std::vector<UnpackJob>& jobs, const uint8_t* h1
   });
 }
 
+// ---- the compact export record (include/biogarden_gpu.h bg_batch_export_compact) expanded on
+// the host into bg_batch_fetch's output, over the pool.  Every header is range-checked against
+// its pair before any byte is written; returns BG_OK or BG_E_ARG.
+inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uint8_t* const* s1,
+                          const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                          bg_pair_result* res, uint8_t* out1, uint8_t* out2, size_t out_cap) {
+  if (!rec || bytes < 32 || (np && (!res || !n1 || !n2 || !s1 || !s2))) return BG_E_ARG;
+  uint64_t head[4];
+  std::memcpy(head, rec, 32);
+  if (head[0] != 0x31434742ull || head[1] != np) return BG_E_ARG;
+  const uint64_t opsBytes = head[2];
+  if (bytes < 32 + np * sizeof(bg_compact_hdr) + opsBytes) return BG_E_ARG;
+  const uint8_t* ops = rec + 32 + np * sizeof(bg_compact_hdr);
+  std::vector<bg_compact_hdr> hd(np);
+  if (np) std::memcpy(hd.data(), rec + 32, np * sizeof(bg_compact_hdr));
+  std::vector<uint64_t> off(np + 1, 0);
+  for (size_t p = 0; p < np; ++p) off[p + 1] = off[p] + n1[p] + n2[p];
+  if (off[np] && (!out1 || !out2 || out_cap < off[np])) return BG_E_ARG;
+  for (size_t p = 0; p < np; ++p) {
+    const bg_compact_hdr& h = hd[p];
+    const uint64_t ncore = (uint64_t)h.len - h.npre - h.ntail;
+    if ((uint64_t)h.npre + h.ntail > h.len || h.len > n1[p] + n2[p] || h.ops_off + (ncore + 3) / 4 > opsBytes ||
+        h.start1 > n1[p] || h.start2 > n2[p] || h.end_i > n1[p] || h.end_j > n2[p] ||
+        (n1[p] && !s1[p]) || (n2[p] && !s2[p]))
+      return BG_E_ARG;
+    // the core consumes exactly s1[start1, end_i) and s2[start2, end_j)
+    uint64_t c1 = 0, c2 = 0;
+    for (uint64_t x = 0; x < ncore; ++x) {
+      const int op = (ops[h.ops_off + x / 4] >> (2 * (x % 4))) & 3;
+      if (op == 3) return BG_E_ARG;
+      c1 += op != 2;
+      c2 += op != 1;
+    }
+    if (h.start1 + c1 != h.end_i || h.start2 + c2 != h.end_j) return BG_E_ARG;
+    const bool colcase = h.end_i < n1[p];
+    if (h.npre && (colcase ? h.npre > n1[p] : h.npre > n2[p])) return BG_E_ARG;
+    if (h.ntail && (colcase ? h.end_i + h.ntail > n1[p] : h.end_j + h.ntail > n2[p])) return BG_E_ARG;
+  }
+  par_ranges(np, [&](size_t p) -> uint64_t { return 2ull * hd[p].len + 64; }, [&](size_t lo, size_t hi) {
+    for (size_t p = lo; p < hi; ++p) {
+      const bg_compact_hdr& h = hd[p];
+      bg_pair_result& o = res[p];
+      std::memset(&o, 0, sizeof(o));
+      o.status = h.status; o.score = h.score; o.offset = off[p]; o.len = h.len;
+      o.end_i = h.end_i; o.end_j = h.end_j; o.start1 = h.start1; o.start2 = h.start2;
+      uint8_t* a1 = out1 + off[p];
+      uint8_t* a2 = out2 + off[p];
+      const bool colcase = h.end_i < n1[p];
+      uint64_t x = 0;
+      for (uint32_t q = 0; q < h.npre; ++q, ++x) {
+        a1[x] = colcase ? s1[p][q] : (uint8_t)'-';
+        a2[x] = colcase ? (uint8_t)'-' : s2[p][q];
+      }
+      const uint64_t ncore = (uint64_t)h.len - h.npre - h.ntail;
+      size_t i = h.start1, j = h.start2;
+      for (uint64_t q = 0; q < ncore; ++q, ++x) {
+        const int op = (ops[h.ops_off + q / 4] >> (2 * (q % 4))) & 3;
+        a1[x] = op != 2 ? s1[p][i++] : (uint8_t)'-';
+        a2[x] = op != 1 ? s2[p][j++] : (uint8_t)'-';
+      }
+      for (uint32_t q = 0; q < h.ntail; ++q, ++x) {
+        a1[x] = colcase ? s1[p][h.end_i + q] : (uint8_t)'-';
+        a2[x] = colcase ? (uint8_t)'-' : s2[p][h.end_j + q];
+      }
+    }
+  });
+  return BG_OK;
+}
+
 }  // namespace bgh

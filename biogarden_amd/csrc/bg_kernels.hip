@@ -431,6 +431,7 @@ __global__ __launch_bounds__(256) void bg_global_score_kernel(BgFinishArgs F) {
   res.status = 0; res.score = score; res.end_i = P.n1; res.end_j = P.n2;
   res.out_start = (uint32_t)(P.n1 + P.n2); res.out_len = 0;
   res.start1 = (uint32_t)P.n1; res.start2 = (uint32_t)P.n2;
+  res.npre = 0; res.ntail = 0;
   F.results[P.index] = res;
 }
 extern "C" void* bg_global_score_kernel_ptr() { return (void*)&bg_global_score_kernel; }
@@ -466,6 +467,77 @@ __global__ __launch_bounds__(256) void bg_export_kernel(BgExportArgs E) {
 }
 
 extern "C" void* bg_export_kernel_ptr() { return (void*)&bg_export_kernel; }
+
+// ------------------------------------------------------------------ compact export (§8(e) gather)
+// Three launches on the handle's stream: per caller pair its header from the template and its
+// packed-ops size (plan pairs from their results); one workgroup's exclusive scan of the sizes
+// into offsets; per plan pair its header and ops copied into the record.
+__global__ __launch_bounds__(256) void bg_compact_size_kernel(BgCompactArgs E) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;   // sizes zeroed by the host
+  if (p >= (uint64_t)E.nplan) return;
+  const BgPair& P = E.pairs[p];
+  const BgResult& r = E.results[P.index];
+  const uint32_t ncore = r.out_len - r.npre - r.ntail;
+  E.sizes[P.caller] = (ncore + 3) / 4;
+}
+
+__global__ __launch_bounds__(1024) void bg_compact_scan_kernel(BgCompactArgs E) {
+  __shared__ uint64_t part[1024];
+  const uint64_t n = E.npairs_caller;
+  const uint64_t per = (n + blockDim.x - 1) / blockDim.x;
+  const uint64_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
+  uint64_t s = 0;
+  for (uint64_t p = lo; p < hi; ++p) s += E.sizes[p];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    for (unsigned t = 0; t < blockDim.x; ++t) { const uint64_t v = part[t]; part[t] = acc; acc += v; }
+    E.sizes[n] = acc;
+  }
+  __syncthreads();
+  uint64_t acc = part[threadIdx.x];
+  for (uint64_t p = lo; p < hi; ++p) { const uint64_t v = E.sizes[p]; E.sizes[p] = acc; acc += v; }
+}
+
+__global__ __launch_bounds__(256) void bg_compact_write_kernel(BgCompactArgs E) {
+  uint64_t* head = reinterpret_cast<uint64_t*>(E.dst);
+  BgCompactHdr* hdr = reinterpret_cast<BgCompactHdr*>(E.dst + 32);
+  uint8_t* opsArea = E.dst + 32 + E.npairs_caller * sizeof(BgCompactHdr);
+  if (blockIdx.x >= (unsigned)E.nplan) {
+    // caller pairs never planned (statuses decided on the host): the template's status
+    const uint64_t base = (uint64_t)(blockIdx.x - E.nplan) * blockDim.x + threadIdx.x;
+    if (base < E.npairs_caller) {
+      const BgPairResultDev& t = E.recs[base];
+      BgCompactHdr o;
+      o.status = t.status; o.score = 0; o.ops_off = E.sizes[base]; o.len = 0; o.end_i = 0; o.end_j = 0;
+      o.start1 = 0; o.start2 = 0; o.npre = 0; o.ntail = 0; o.reserved = 0;
+      // planned pairs are written by their own workgroups (after this one may have run): only
+      // pairs whose template status marks them as decided on the host
+      if (t.status != 0) hdr[base] = o;
+    }
+    if (base == 0) { head[0] = 0x31434742ull;   /* "BGC1" */ head[1] = E.npairs_caller; head[2] = E.sizes[E.npairs_caller]; head[3] = (uint64_t)E.mode; }
+    return;
+  }
+  const BgPair& P = E.pairs[blockIdx.x];
+  const BgResult& r = E.results[P.index];
+  const uint32_t nb = (r.out_len - r.npre - r.ntail + 3) / 4;
+  const uint64_t off = E.sizes[P.caller];
+  for (uint32_t x = threadIdx.x; x < nb; x += blockDim.x) opsArea[off + x] = E.ops[P.ops_off + x];
+  if (threadIdx.x == 0) {
+    BgCompactHdr o;
+    o.status = r.status;
+    if (o.status == 0 && bg_ref_divergent(E.mode, P.n1, P.n2, r.score, P.buf_rows, P.buf_cols)) o.status = 4;
+    o.score = r.score; o.ops_off = off; o.len = r.out_len;
+    o.end_i = (uint32_t)r.end_i; o.end_j = (uint32_t)r.end_j; o.start1 = r.start1; o.start2 = r.start2;
+    o.npre = r.npre; o.ntail = r.ntail; o.reserved = 0;
+    hdr[P.caller] = o;
+  }
+}
+
+extern "C" void* bg_compact_size_kernel_ptr() { return (void*)&bg_compact_size_kernel; }
+extern "C" void* bg_compact_scan_kernel_ptr() { return (void*)&bg_compact_scan_kernel; }
+extern "C" void* bg_compact_write_kernel_ptr() { return (void*)&bg_compact_write_kernel; }
 
 // Residue coding on the device: codes[x] = lut[raw[x]] over both concatenated sequence sets
 // (the host uploads only the raw bytes, which the strings are built from anyway).  16 bytes per

@@ -2,8 +2,10 @@
 
 One process per GPU.  A batch is split over ranks by cells (largest-first greedy, like the
 in-GPU pair plan); every rank runs its shard through its own `bg_aligner`, packs the results
-on the device with `bg_batch_export`, and rank 0 collects the packed records with one
-variable-size gather (RCCL over xGMI with backend "nccl", gloo on CPU).  No collective is on
+on the device — `bg_batch_export_compact`: headers plus the alignment cores as 2-bit edit
+scripts, 10-250x smaller than the strings — and rank 0 collects the records with one
+variable-size gather (RCCL send/recv over xGMI with backend "nccl", gloo on CPU) and expands
+them into aligned strings on the host (`_native.expand_compact`, which has the input sequences).  No collective is on
 the data path: the pairs' answers share nothing (reference: one `SequenceAligner` call per
 pair, src/alignment/aligner.rs:84-435).
 
@@ -87,20 +89,34 @@ def encode_export(results):
 
 
 def gather_packed(local, dist, dst=0):
-    """Variable-size gather of one uint8 tensor per rank to `dst`.  Returns, on dst, the list of
-    per-rank byte strings (rank order); None elsewhere.  `local` lives on the device the
-    process group communicates on (cuda for RCCL, cpu for gloo)."""
+    """Variable-size gather of one uint8 tensor per rank to `dst`: the sizes by one all_gather,
+    then every other rank sends exactly its bytes to `dst` (point-to-point, RCCL send/recv over
+    xGMI with backend "nccl"; gloo on CPU) — no rank is padded to the largest.  Returns, on dst,
+    the list of per-rank byte strings (rank order); None elsewhere.  `local` lives on the device
+    the process group communicates on (cuda for RCCL, cpu for gloo)."""
     import torch
     world = dist.get_world_size()
+    rank = dist.get_rank()
     dev = local.device
     n = torch.tensor([local.numel()], dtype=torch.int64, device=dev)
     sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(sizes, n)
-    mx = int(max(int(s.item()) for s in sizes))
-    buf = torch.zeros(max(mx, 1), dtype=torch.uint8, device=dev)
-    buf[:local.numel()] = local
-    gl = [torch.empty_like(buf) for _ in range(world)] if dist.get_rank() == dst else None
-    dist.gather(buf, gl, dst=dst)
-    if dist.get_rank() != dst:
+    sz = [int(s.item()) for s in sizes]
+    if rank != dst:
+        if sz[rank]:
+            for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), dst)]):
+                w.wait()
         return None
-    return [g[:int(s.item())].cpu().numpy().tobytes() for g, s in zip(gl, sizes)]
+    bufs = [None] * world
+    ops = []
+    for r in range(world):
+        if r == dst:
+            bufs[r] = local
+        else:
+            bufs[r] = torch.empty(sz[r], dtype=torch.uint8, device=dev)
+            if sz[r]:
+                ops.append(dist.P2POp(dist.irecv, bufs[r], r))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return [b.cpu().numpy().tobytes() if b.numel() else b"" for b in bufs]

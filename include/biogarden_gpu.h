@@ -187,6 +187,29 @@ int bg_aligner_set_call_dims(bg_aligner* h, size_t npairs, const uint64_t* rows,
 int bg_profile_begin(bg_aligner* h);
 int bg_profile_end(bg_aligner* h, float* avg_dp_ms, float* avg_finish_ms, int* executes);
 
+/* Compact export of the last execute's results, the payload of the multi-GPU gather (SURVEY
+ * §8(e)): per caller pair a header, then the alignment cores as edit scripts, 2 bits per column
+ * (0 = (s1, s2), 1 = (s1, '-'), 2 = ('-', s2)), back to back:
+ *   [u64 "BGC1"][u64 npairs][u64 ops bytes][u64 mode][bg_compact_hdr x npairs][ops]
+ * A pair's strings are npre prefix columns (semiglobal: s1[0, npre) against gaps when end_i < n1,
+ * else s2[0, npre)), the core's columns consuming s1 from start1 and s2 from start2, and ntail
+ * tail columns (s1[end_i, ...) against gaps when end_i < n1, else s2[end_j, ...)); len counts all
+ * of them.  bg_compact_expand rebuilds bg_batch_fetch's output from it and the input sequences.
+ * dst = NULL: computes the record on the device (waits for the execute) and returns its exact
+ * size in *bytes; then call again with dst (device memory of the handle's GPU, *bytes >= size). */
+typedef struct bg_compact_hdr {
+  int32_t status, score;
+  uint64_t ops_off;  /* into the ops area */
+  uint32_t len, end_i, end_j, start1, start2, npre, ntail, reserved;
+} bg_compact_hdr;
+int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes);
+/* Host-only: expands a compact record (rec_bytes bytes in host memory) of npairs pairs into the
+ * form bg_batch_fetch returns for the same pairs (results, out1 / out2 at offset sum of n1 + n2 over
+ * earlier pairs, out_cap >= that sum).  BG_E_ARG if the record does not match the pairs. */
+int bg_compact_expand(const void* rec, size_t rec_bytes, size_t npairs, const uint8_t* const* s1,
+                      const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                      bg_pair_result* results, uint8_t* out1, uint8_t* out2, size_t out_cap);
+
 /* Host-side time of this handle's bg_batch_prepare / bg_batch_fetch calls, accumulated (ms):
  *   ms[0] waiting for the handle's previous work   ms[1] validation + staging (byte pass)
  *   ms[2] planning (history, alphabet, geometry)   ms[3] device allocation

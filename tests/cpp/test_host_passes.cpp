@@ -162,6 +162,105 @@ int main() {
     const size_t big[] = {(size_t)1 << 30};
     CHECK(bgh::stage_validate(BG_GLOBAL, 1, p2, big, p2, n2, -1, -1, pre, c1, c2) == BG_E_ARG);
   }
-  std::printf("host passes ok (%d batches)\n", batches);
+  // compact export records (bg_batch_export_compact's format): random alignments encoded as
+  // headers + 2-bit cores, expanded, checked against a direct construction; malformed records
+  // (bad magic, truncation, op 3, inconsistent consumption, out-of-range fields) are refused
+  int records = 0;
+  for (int it = 0; it < 60; ++it) {
+    setenv("BG_HOST_THREADS", threads[it % 3], 1);
+    const size_t np = rng() % 30;
+    std::vector<std::string> a(np), b(np), w1(np), w2(np);
+    std::vector<bg_compact_hdr> hd(np);
+    std::vector<uint8_t> ops;
+    for (size_t p = 0; p < np; ++p) {
+      const size_t n1 = rng() % 300, n2 = rng() % 300;
+      a[p].resize(n1); b[p].resize(n2);
+      for (auto& c : a[p]) c = (char)(rng() % 256);      // any byte, '-' included
+      for (auto& c : b[p]) c = (char)(rng() % 256);
+      bg_compact_hdr h;
+      std::memset(&h, 0, sizeof(h));
+      h.status = (int)(rng() % 5);
+      h.score = (int)(rng() % 1000) - 500;
+      // a core from (s1, s2) to (e1, e2), then optional semiglobal prefix / tail runs
+      size_t s1 = n1 ? rng() % (n1 + 1) : 0, s2 = n2 ? rng() % (n2 + 1) : 0;
+      size_t i = s1, j = s2;
+      std::vector<int> core;
+      while ((i < n1 || j < n2) && rng() % 50) {
+        int op = (int)(rng() % 3);
+        if (op != 2 && i >= n1) op = 2;
+        if (op != 1 && j >= n2) op = (i < n1) ? 1 : -1;
+        if (op < 0) break;
+        core.push_back(op);
+        i += op != 2;
+        j += op != 1;
+      }
+      h.start1 = (uint32_t)s1; h.start2 = (uint32_t)s2; h.end_i = (uint32_t)i; h.end_j = (uint32_t)j;
+      const bool colcase = i < n1;
+      h.npre = (uint32_t)(rng() % 2 ? 0 : (colcase ? (n1 ? rng() % (n1 + 1) : 0) : (n2 ? rng() % (n2 + 1) : 0)));
+      h.ntail = (uint32_t)(rng() % 2 ? 0 : (colcase ? rng() % (n1 - i + 1) : rng() % (n2 - j + 1)));
+      h.len = (uint32_t)(h.npre + core.size() + h.ntail);
+      if (h.len > n1 + n2) { h.npre = 0; h.ntail = 0; h.len = (uint32_t)core.size(); }
+      h.ops_off = ops.size();
+      for (size_t q = 0; q < core.size(); q += 4) {
+        uint8_t v = 0;
+        for (size_t r = 0; r < 4 && q + r < core.size(); ++r) v |= (uint8_t)(core[q + r] << (2 * r));
+        ops.push_back(v);
+      }
+      // the expected strings
+      for (uint32_t q = 0; q < h.npre; ++q) {
+        w1[p] += colcase ? a[p][q] : '-';
+        w2[p] += colcase ? '-' : b[p][q];
+      }
+      size_t ii = s1, jj = s2;
+      for (int op : core) { w1[p] += op != 2 ? a[p][ii++] : '-'; w2[p] += op != 1 ? b[p][jj++] : '-'; }
+      for (uint32_t q = 0; q < h.ntail; ++q) {
+        w1[p] += colcase ? a[p][i + q] : '-';
+        w2[p] += colcase ? '-' : b[p][j + q];
+      }
+      hd[p] = h;
+    }
+    std::vector<uint8_t> rec(32 + np * sizeof(bg_compact_hdr) + ops.size());
+    const uint64_t head[4] = {0x31434742ull, np, ops.size(), 4};
+    std::memcpy(rec.data(), head, 32);
+    if (np) std::memcpy(rec.data() + 32, hd.data(), np * sizeof(bg_compact_hdr));
+    if (!ops.empty()) std::memcpy(rec.data() + 32 + np * sizeof(bg_compact_hdr), ops.data(), ops.size());
+    std::vector<const uint8_t*> p1(np), p2(np);
+    std::vector<size_t> n1(np), n2(np);
+    size_t cap = 0;
+    for (size_t p = 0; p < np; ++p) {
+      p1[p] = reinterpret_cast<const uint8_t*>(a[p].data()); n1[p] = a[p].size();
+      p2[p] = reinterpret_cast<const uint8_t*>(b[p].data()); n2[p] = b[p].size();
+      cap += n1[p] + n2[p];
+    }
+    std::vector<bg_pair_result> res(np + 1);
+    std::vector<uint8_t> o1(cap + 1), o2(cap + 1);
+    CHECK(bgh::compact_expand(rec.data(), rec.size(), np, p1.data(), n1.data(), p2.data(), n2.data(),
+                              res.data(), o1.data(), o2.data(), cap) == BG_OK);
+    size_t off = 0;
+    for (size_t p = 0; p < np; ++p) {
+      CHECK(res[p].offset == off && res[p].len == hd[p].len && res[p].status == hd[p].status);
+      CHECK(std::string(reinterpret_cast<char*>(o1.data() + off), res[p].len) == w1[p]);
+      CHECK(std::string(reinterpret_cast<char*>(o2.data() + off), res[p].len) == w2[p]);
+      off += n1[p] + n2[p];
+    }
+    // malformed: truncated, bad magic, and one corrupted header field
+    if (np) {
+      CHECK(bgh::compact_expand(rec.data(), rec.size() - 1, np, p1.data(), n1.data(), p2.data(), n2.data(),
+                                res.data(), o1.data(), o2.data(), cap) == BG_E_ARG);
+      std::vector<uint8_t> bad = rec;
+      bad[0] ^= 1;
+      CHECK(bgh::compact_expand(bad.data(), bad.size(), np, p1.data(), n1.data(), p2.data(), n2.data(),
+                                res.data(), o1.data(), o2.data(), cap) == BG_E_ARG);
+      bad = rec;
+      bg_compact_hdr h0;
+      std::memcpy(&h0, bad.data() + 32, sizeof(h0));
+      h0.end_i += 1;                                   // consumption no longer matches
+      std::memcpy(bad.data() + 32, &h0, sizeof(h0));
+      CHECK(bgh::compact_expand(bad.data(), bad.size(), np, p1.data(), n1.data(), p2.data(), n2.data(),
+                                res.data(), o1.data(), o2.data(), cap) == BG_E_ARG);
+    }
+    ++records;
+  }
+  std::printf("host passes ok (%d batches, %d compact records)\n", batches, records);
   return 0;
 }

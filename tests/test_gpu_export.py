@@ -132,3 +132,84 @@ def test_call_dims_mismatch_is_rejected():
         h.prepare("global", _pairs(1, n=2), _native.builtin_scoring(_native.BG_BLOSUM62), -11, -1)
     finally:
         h.close()
+
+
+def _compact(h):
+    import torch
+    n = h.export_compact_size()
+    buf = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
+    h.export_compact_to(buf.data_ptr(), n)
+    torch.cuda.synchronize()
+    return buf[:n].cpu().numpy().tobytes()
+
+
+@pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("semiglobal", -11, -1), ("global", -11, -1),
+                                      ("local", -11, -1), ("fitting", -1, -1), ("overlap", -2, -2)])
+def test_compact_export_expands_to_fetch(mode, a, b):
+    """bg_batch_export_compact (headers + 2-bit edit scripts of the alignment cores, the gather
+    payload) expanded on the host with the input sequences = bg_batch_fetch, pair for pair:
+    semiglobal prefixes / tails, empty and unscorable pairs (status 3), divergence flags."""
+    from biogarden_amd import _native
+    pairs = _pairs(23 + len(mode) + a)
+    pairs += [(b"ACGTNNACGT", b"ACGT"), (b"", b"ACG"), (b"A", b""), (b"ACGTZACGT", b"ACGT")]
+    pairs += [(b"ACGT" * 40, b"AC!GT")]                     # '!' is outside score.rs's table: status 3
+    h = _native.Handle(0)
+    try:
+        h.prepare(mode, pairs, _native.builtin_scoring(_native.BG_BLOSUM62), a, b)
+        h.execute()
+        fetched = h.fetch()
+        rec = _compact(h)
+    finally:
+        h.close()
+    assert _native.expand_compact(rec, pairs) == fetched
+    assert any(r["status"] == 3 for r in fetched)
+    full = 8 + 40 * len(pairs) + 2 * sum(len(x) + len(y) for x, y in pairs)
+    assert len(rec) < full / 4, (len(rec), full)
+
+
+def test_compact_export_with_gap_byte_residues():
+    """A closure over raw bytes where '-' itself is a residue (the reference's scorer is any
+    &dyn Fn(&u8, &u8) -> i32): the edit script, not the strings, carries the gaps, so the
+    expansion is still exact."""
+    from biogarden_amd import _native
+    from biogarden_amd.alignment import score
+    alpha = b"-ACGT"
+    rng = random.Random(8)
+    pairs = []
+    for n1, n2 in ((300, 280), (64, 65), (1000, 700), (5, 0)):
+        s1 = rand_seq(rng, n1, alpha)
+        pairs.append((s1, mutate(rng, s1, alpha, 0.2)[:n2]))
+    sc, _ = score.tabulate(lambda x, y: 5 if x == y else -4, pairs)
+    h = _native.Handle(0)
+    try:
+        h.prepare("global", pairs, sc, -6, -1)
+        h.execute()
+        fetched = h.fetch()
+        rec = _compact(h)
+    finally:
+        h.close()
+    assert _native.expand_compact(rec, pairs) == fetched
+    assert any(b"-" in x for x, _ in pairs)
+
+
+def test_compact_gather_over_rccl_world1():
+    import torch
+    import torch.distributed as dist
+    from biogarden_amd import _native, shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    pairs = _pairs(31)
+    h = _native.Handle(0)
+    try:
+        h.prepare("semiglobal", pairs, _native.builtin_scoring(_native.BG_BLOSUM62), -1, -2)
+        h.execute()
+        fetched = h.fetch()
+        n = h.export_compact_size()
+        buf = torch.empty(max(n, 1), dtype=torch.uint8, device="cuda")
+        h.export_compact_to(buf.data_ptr(), n)
+        got = shard.gather_packed(buf[:n], dist, dst=0)
+        assert _native.expand_compact(got[0], pairs) == fetched
+    finally:
+        h.close()
+        dist.destroy_process_group()
