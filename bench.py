@@ -297,6 +297,20 @@ def cpu_section(pairs, gpu_scores, mode, a, b, info, pairs_multi, pairs_one):
         out["C1_one_core"] = {"value": round(r1, 4), "seconds": round(s1_, 3), "score": sc1[0],
                               "cells": workloads.cells(c1),
                               "config": "semiglobal_alignment.fasta 9559x8457, blosum62 -1/-2"}
+        # C3 (100 kbp x 100 kbp) on the CPU needs the reference's 150 GB of matrices and ~80 s:
+        # too long for this line; extrapolated from C1's in-run 1-core rate, with the measured
+        # run of tools/c3_cpu.py on an MI355X box beside it (strings equal to the GPU's)
+        c3 = {"extrapolated_seconds": round(1e10 / (r1 * 1e9), 1),
+              "basis": "1e10 cells at this run's C1 one-core rate"}
+        try:
+            with open(os.path.join(ROOT, "profiles", "r03", "c3_cpu.json")) as f:
+                m = json.loads(f.read())
+            c3["measured_record"] = {"file": "profiles/r03/c3_cpu.json", "seconds": m.get("cpu_seconds"),
+                                     "gcups_one_core": m.get("cpu_gcups_one_core"),
+                                     "strings_equal_gpu": m.get("strings_equal")}
+        except (OSError, ValueError):
+            pass
+        out["C3_one_core"] = c3
     except (OSError, IndexError, ImportError):
         pass
     return out
