@@ -98,7 +98,7 @@ struct BgDpArgs {
   int32_t npairs;
   int32_t prog_off;        // byte offset of the 16 per-wave progress counters in dynamic LDS
   int32_t codes_off;       // byte offset of the staged seq2 codes in dynamic LDS
-  int32_t codes_in_lds;    // 1 if every pair's seq2 fits there
+  int32_t codes_in_lds;    // 1 if every pair's seq2 fits there; 2: tagged WIDE, 2-bit packed row
   int32_t aux_lds_off;     // tagged kernel: per-wave area (boundary block, ring, profile, codes)
   const int2* wgmap;       // tagged kernel, WIDE mode: per workgroup (plan index, index in group)
   uint32_t* gprog;         // tagged kernel, WIDE mode: global per-wave progress counters
@@ -106,6 +106,10 @@ struct BgDpArgs {
   unsigned long long* dbg; // optional per-wave timestamps of the first strip (env BG_DP_TIMING):
                            // [gw * 8 + k], k: 0 strip, 1 start, 2 chunk 0 done, 3 end, 4 waited
   int32_t* prof_scratch;   // mask kernel, int32 profiles in HBM: kdim x 64 x R ints per (pair, wave)
+  unsigned long long* gran;  // tagged WIDE checkpoint mode: strip-boundary rows as {value, epoch}
+                             // granules, indexed like bndM (zeroed when allocated)
+  uint32_t epoch;          // this execute's granule tag (never 0, never reused by the handle)
+  int32_t wide_pace;       // WIDE: s_sleep(1)s strip 0 adds per 32 steps (slack for the chain)
 };
 
 struct BgFinishArgs {

@@ -130,7 +130,7 @@ struct PhaseTimer {
 // Per-execute arenas.  Two slots let the finish kernel of execute k (stream2) run while the
 // DP kernel of execute k+1 (stream) fills the other slot's trace.
 struct Slot {
-  DevBuf trace, bndM, bndX, aux, out1, out2, results, ops;
+  DevBuf trace, bndM, bndX, aux, out1, out2, results, ops, gran;
   hipEvent_t dpDone = nullptr, finDone = nullptr;
   bool inflight = false;
 };
@@ -141,12 +141,14 @@ struct bg_aligner {
   hipStream_t stream = nullptr;    // uploads, DP kernels, downloads
   hipStream_t stream2 = nullptr;   // end cell + traceback kernels
   hipStream_t stream3 = nullptr;   // WIDE batches: every other execute's traceback (see execute)
+  hipStream_t stream4 = nullptr;   // WIDE batches at pipeline depth 4: every third one
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
   DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
   Slot slot[4];
   int depth = 3;                   // pipeline depth: arena slots in flight (1..4; 3 lets the
                                    // traceback of step k overlap the DPs of k+1 and k+2)
   int execCount = 0;
+  uint32_t epoch = 0;              // WIDE granule tag of the last execute (never reset)
   int lastSlot = 0;
 
   // profiling ring (bg_profile_begin/end)
@@ -219,7 +221,7 @@ struct bg_aligner {
                profScratch.cap;
     for (const Slot& S : slot)
       t += S.trace.cap + S.bndM.cap + S.bndX.cap + S.aux.cap + S.out1.cap + S.out2.cap + S.results.cap +
-           S.ops.cap;
+           S.ops.cap + S.gran.cap;
     return t;
   }
 };
@@ -278,7 +280,8 @@ extern "C" bg_aligner* bg_aligner_new(int device) {
     h->cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream4, hipStreamNonBlocking) != hipSuccess) {
     bg_aligner_free(h);
     return nullptr;
   }
@@ -299,12 +302,13 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   if (h->stream3) (void)hipStreamSynchronize(h->stream3);
+  if (h->stream4) (void)hipStreamSynchronize(h->stream4);
   for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs,
                     &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg, &h->profScratch, &h->compactSizes})
     d->release();
   for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
   for (Slot& S : h->slot) {
-    for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops}) d->release();
+    for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops, &S.gran}) d->release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
     if (S.finDone) (void)hipEventDestroy(S.finDone);
   }
@@ -315,6 +319,7 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   if (h->stream) (void)hipStreamDestroy(h->stream);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->stream3) (void)hipStreamDestroy(h->stream3);
+  if (h->stream4) (void)hipStreamDestroy(h->stream4);
   delete h;
 }
 
@@ -339,7 +344,8 @@ extern "C" int bg_set_kernel_options(bg_aligner* h, int allow_tagged) {
 extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
   if (!h || depth < 1 || depth > 4) return BG_E_ARG;
   if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
-      hipStreamSynchronize(h->stream2) != hipSuccess || hipStreamSynchronize(h->stream3) != hipSuccess)
+      hipStreamSynchronize(h->stream2) != hipSuccess || hipStreamSynchronize(h->stream3) != hipSuccess ||
+      hipStreamSynchronize(h->stream4) != hipSuccess)
     return BG_E_HIP;
   h->depth = depth;
   h->prepared = false;   // arenas are sized at prepare time
@@ -672,6 +678,7 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
+  BG_HIP(hipStreamSynchronize(h->stream4));
   tm.mark(kPhSync, "sync");
   for (Slot& S : h->slot) S.inflight = false;
   h->execCount = 0;
@@ -804,7 +811,12 @@ plan_again:
     const size_t waves = (size_t)W * bg_dp_tag_wave_lds_bytes(R);
     const size_t row = round_up(2 * (64 + (maxn2 / 64 + 4) * 64), 16);
     h->codesInLds = (h->tagRow && 640 + row + waves <= 160 * 1024) ? 1 : 0;
-    h->auxLdsOff = (int)(640 + (h->codesInLds ? row : 0));
+    // WIDE pairs whose u16 row does not fit: the row as 2-bit codes (4 columns per byte), so
+    // no chunk of the strip pipeline loads its codes from HBM (a per-chunk load made the
+    // compiler drain the previous chunk's stores at every chunk start)
+    const size_t packed = round_up((size_t)(maxn2 / 64 + 5) * 16, 16);
+    if (!h->codesInLds && h->wide && 640 + packed + waves <= 160 * 1024) h->codesInLds = 2;
+    h->auxLdsOff = (int)(640 + (h->codesInLds == 1 ? row : (h->codesInLds == 2 ? packed : 0)));
     lds = h->auxLdsOff + waves;
     // WIDE: one workgroup (one wave per SIMD) per CU — claim over half of the CU's LDS so the
     // dispatcher cannot stack a group's workgroups on one CU
@@ -937,6 +949,15 @@ plan_again:
         !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) || !S.ops.ensure(po + 16) ||
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)))
       return BG_E_NOMEM;
+    // WIDE checkpoint batches hand strip rows between workgroups as epoch-tagged granules: a
+    // fresh arena is zeroed so that no stale tag (of another handle) can match an epoch
+    if (h->wide && h->tag && h->ckpt) {
+      const size_t gb = bo * 8 + 256;
+      if (S.gran.cap < gb) {
+        if (!S.gran.ensure(gb)) return BG_E_NOMEM;
+        BG_HIP(hipMemset(S.gran.p, 0, S.gran.cap));
+      }
+    }
   }
 
   tm.mark(kPhAlloc, "alloc");
@@ -1104,6 +1125,13 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     }
     if (h->wide) BG_HIP(hipMemsetAsync(h->gprogBuf.p, 0, 4 * (size_t)h->progWords, h->stream));
     A.prof_scratch = h->pglob ? h->profScratch.as<int32_t>() : nullptr;
+    if (++h->epoch == 0) h->epoch = 1;
+    A.epoch = h->epoch;
+    {
+      const char* ev = std::getenv("BG_WIDE_PACE");
+      A.wide_pace = ev ? std::atoi(ev) : 0;
+    }
+    A.gran = S.gran.as<unsigned long long>();
     A.trace = S.trace.as<uint32_t>();
     A.bndM = S.bndM.as<int32_t>();
     A.bndX = S.bndX.as<int32_t>();
@@ -1127,10 +1155,14 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   // and run side by side (each still waits for its own DP; the slot it reads is not reused before
   // its finDone); the step then follows the DP.  Many-pair batches keep one stream: their finish
   // workgroups fill the CUs beside the next DP as it is.
-  hipStream_t fs = h->stream2;
-  if ((h->wide || std::getenv("BG_TWO_FIN_STREAMS")) && (h->execCount & 1) && !std::getenv("BG_FINISH_TIMING") &&
+  // At pipeline depth 4 a WIDE batch's tracebacks rotate over three streams: a C3 walk (one
+  // latency-bound workgroup, ~13 ms) then hides behind three DPs instead of two.
+  int nfs = 1;
+  if ((h->wide || std::getenv("BG_TWO_FIN_STREAMS")) && !std::getenv("BG_FINISH_TIMING") &&
       !std::getenv("BG_ONE_FIN_STREAM"))
-    fs = h->stream3;
+    nfs = h->wide ? std::min(3, std::max(2, h->depth - 1)) : 2;
+  const hipStream_t fss[3] = {h->stream2, h->stream3, h->stream4};
+  hipStream_t fs = fss[h->execCount % nfs];
   BG_HIP(hipStreamWaitEvent(fs, S.dpDone, 0));
   BG_HIP(hipEventRecord(e[2], fs));
   if (np) {
@@ -1217,6 +1249,7 @@ extern "C" int bg_synchronize(bg_aligner* h) {
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
+  BG_HIP(hipStreamSynchronize(h->stream4));
   if (h->executed) {
     (void)hipEventElapsedTime(&h->dp_ms, h->last[0], h->last[1]);
     (void)hipEventElapsedTime(&h->fin_ms, h->last[2], h->last[3]);
@@ -1414,6 +1447,7 @@ extern "C" int bg_profile_end(bg_aligner* h, float* avg_dp, float* avg_fin, int*
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
+  BG_HIP(hipStreamSynchronize(h->stream4));
   double dp = 0, fin = 0;
   const int cnt = h->ringUsed / 4;
   for (int i = 0; i < cnt; ++i) {
@@ -1440,6 +1474,7 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
+  BG_HIP(hipStreamSynchronize(h->stream4));
   const Slot& S = h->slot[h->lastSlot];
   const uint64_t n = h->npairs;
   BG_HIP(hipMemcpyAsync(dst, &n, 8, hipMemcpyHostToDevice, h->stream));
@@ -1486,6 +1521,7 @@ extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) 
     E.dst = nullptr;
     BG_HIP(hipStreamSynchronize(h->stream2));
     BG_HIP(hipStreamSynchronize(h->stream3));
+    BG_HIP(hipStreamSynchronize(h->stream4));
     BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), h->stream));
     const unsigned g = (unsigned)(((uint64_t)E.nplan + 255) / 256);
     if (g) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(g), dim3(256), args, 0, h->stream));

@@ -289,8 +289,9 @@ __device__ __forceinline__ int dpp_shl1(int old, int src) {
 //   * after 64 steps Q[r] = the last row at column t0 - 64 + r: block c - 1, final, ready to go to
 //     the consumer.  The caller stores it and loads the next incoming block.
 // Only the last strip, whose output row is row n1 (any lane), keeps the ring (score_chunk).
-template <int R, int VAR>
-__device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C, int c, int& Q) {
+// `mid` runs between the chunk's two halves (the kernel's HBM hand-offs).
+template <int R, int VAR, class Mid>
+__device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C, int c, int& Q, Mid&& mid) {
   const int a = C.a;
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
@@ -349,6 +350,10 @@ __device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C
           }
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (h == 0) {
+      mid();
       __builtin_amdgcn_sched_barrier(0);
     }
   }

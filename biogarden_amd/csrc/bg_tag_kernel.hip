@@ -121,12 +121,28 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   // the pair's whole scaled code row, when it fits (A.codes_in_lds): 64 zero entries before it
   // and zeros past n2 up to (NC + 2) chunks; else codes are staged per wave and chunk
   uint16_t* sRow = reinterpret_cast<uint16_t*>(smem + A.codes_off) + 64;
-  if (A.codes_in_lds) {
+  // WIDE pairs too long for that: 2-bit codes, byte p = columns 4p - 64 .. 4p - 61 (0 outside
+  // the row), unpacked into the wave's stage once per chunk
+  uint8_t* sPk = smem + A.codes_off;
+  if (A.codes_in_lds == 1) {
     const BgPair& Pp = A.pairs[pairIdx];
     const uint8_t* g = A.codes2 + Pp.off2;
     const int n = (Pp.nc + 2) * BG_CHUNK;
     for (int x = (int)threadIdx.x - 64; x < n; x += blockDim.x)
       sRow[x] = (x >= 0 && x < Pp.n2) ? (uint16_t)(g[x] * (32 * RW)) : (uint16_t)0;
+  } else if (WIDE && A.codes_in_lds == 2) {
+    const BgPair& Pp = A.pairs[pairIdx];
+    const uint8_t* g = A.codes2 + Pp.off2;   // code * 8
+    const int nb = (Pp.nc + 3) * 16;
+    for (int p = threadIdx.x; p < nb; p += blockDim.x) {
+      unsigned v = 0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int x = 4 * p - 64 + k;
+        if (x >= 0 && x < Pp.n2) v |= ((unsigned)g[x] >> 3) << (2 * k);
+      }
+      sPk[p] = (uint8_t)v;
+    }
   }
   __syncthreads();
 
@@ -155,7 +171,8 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
   C.mail = nullptr;
   C.ring = waveLds + 64;
   C.profLane = reinterpret_cast<const uint8_t*>(profTab + lane * RW);
-  const bool rowInLds = A.codes_in_lds != 0;
+  const bool rowInLds = A.codes_in_lds == 1;
+  const bool rowPacked = WIDE && A.codes_in_lds == 2;
   C.codeLane = stage + 63 - lane;       // (t - lane - 1) - (t0 - 64) = u + 63 - lane
 
   const uint8_t* c1 = A.codes1 + P.off1;
@@ -175,6 +192,14 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     for (int q = 0; q < 3; ++q) {
       const int x = c * BG_CHUNK - 64 + lane + 64 * q;
       stage[lane + 64 * q] = (uint16_t)(((unsigned)x < (unsigned)n2) ? v[q] * (32 * RW) : 0);
+    }
+  };
+  // ... or from the packed row in LDS (columns t0 - 64 + lane + 64q: byte 16(c + q) + lane / 4)
+  auto stage_packed = [&](int c) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const unsigned v = sPk[16 * (c + q) + (lane >> 2)];
+      stage[lane + 64 * q] = (uint16_t)(((v >> (2 * (lane & 3))) & 3u) * (256 * RW));
     }
   };
 
@@ -230,7 +255,120 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
                                  (size_t)s * NC * (R + 1) * BG_WAVE + lane
                            : nullptr;
     int cv[3] = {0, 0, 0};
-    if (!rowInLds) fetch_codes(0, cv);
+    if (!rowInLds && !rowPacked) fetch_codes(0, cv);
+    const bool hbmAhead = WIDE && s > 0 && !mailIn;
+    const int pwH = (s - 1) % GW;
+    const int needBase = ((s - 1) / GW) * nblk;
+    const int32_t* bndAbove = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + lane;
+    const bool dbgOn = A.dbg != nullptr && rho == 0 && pairIdx == 0 && gw < 4096;
+    unsigned long long tWait = 0, tStart = dbgOn ? __builtin_amdgcn_s_memrealtime() : 0;
+    const unsigned long long cStart = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
+    // CONV mode (WIDE, checkpoint): every strip but the last runs the one-register conveyor step
+    // (score_chunk_conv) and hands its last row down in HALF blocks of 32 columns, as soon as
+    // each half leaves the conveyor: a consumer then trails its producer by 64 + 32 steps (the
+    // lanes' anti-diagonal skew plus one half) instead of two whole chunks.
+    //  * same workgroup: 32-int half slots of the producer's LDS mailbox (2 kMailSlots of them),
+    //    counters in halves, one sequence per wave across its rounds (seq = rho * nh + half);
+    //  * another workgroup: 8-byte {value, epoch} granules (A.gran, the MI355X guide's data-tagged
+    //    hand-off: one aligned `sc1` store each, read with `sc1` loads until every tag equals
+    //    this launch's epoch) — no counter, no store drain before a publication, and the reader's
+    //    only loads are issued a half ahead, so no wait of this loop waits on a fresh store.
+    // The last strip reads whole blocks (two adjacent half slots, or 64 granules) and keeps the
+    // ring path for its output row (row n1 may sit in any lane).
+    constexpr bool CONVMODE = WIDE && CKPT;
+    constexpr int KH = 2 * kMailSlots;                          // half slots per mailbox
+    const int nh = 2 * nblk;                                     // halves handed down per strip
+    const uint32_t ep = A.epoch;
+    unsigned long long* gOut = A.gran + P.bnd_off + (size_t)s * NC * BG_CHUNK;
+    const unsigned long long* gIn = A.gran + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK;
+    if (CONVMODE && !lastStrip) {
+      const bool lo = lane < 32;
+      const int l32 = lane & 31;
+      const int hb = rho * nh;                                   // this round's half sequence base
+      unsigned long long gv = 0;
+      if (hbmAhead && 0 < nh) gv = __hip_atomic_load(gIn + l32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int Q = 0;
+      // half og of this strip's last row, in lanes 32-63 of v: to the consumer and to bndOut
+      auto emit = [&](int og, int v) {
+        const int col = 32 * og + l32;
+        if (mailOut) {
+          const int sq = hb + og;
+          int np = 0;
+          while (__hip_atomic_load(sCons + w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < sq + 1 - KH)
+            wide_poll_pause(np);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          if (!lo) mailbox[(sq % KH) * 32 + l32] = v;
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);              // LDS: the counter after the data
+          if (lane == 0) __hip_atomic_store(sProg + w, sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (!lo) {
+          __hip_atomic_store(gOut + col, ((unsigned long long)ep << 32) | (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (!lo) __hip_atomic_store(C.bndOut + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      };
+      // before half g: the row above's half g into lanes 0-31 (lane 0 reads it at the next step),
+      // the finished half g - 3 (lanes 32-63) out
+      auto boundary = [&](int g) {
+        const unsigned long long tw0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
+        int inV;
+        if (s == 0) {
+          const int j = 32 * g + l32;
+          inV = wadd(row0_M(mode, j, a, b), -wmul(a, j));                    // M'(0, j)
+          for (int z = 0; z < A.wide_pace; ++z) __builtin_amdgcn_s_sleep(1);
+        } else if (mailIn) {
+          const int sq = hb + g;
+          if (g < nh) {
+            int np = 0;
+            while (__hip_atomic_load(sProg + prevW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < sq + 1)
+              wide_poll_pause(np);
+          }
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          inV = prevMail[(sq % KH) * 32 + l32];
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);              // LDS: the release after the read
+          if (lane == 0) __hip_atomic_store(sCons + w, sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          if (g < nh) {
+            int np = 0;
+            while (!__all(!lo || (uint32_t)(gv >> 32) == ep)) {
+              wide_poll_pause(np);
+              gv = __hip_atomic_load(gIn + 32 * g + l32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
+          inV = (int)(uint32_t)gv;
+          if (g + 1 < nh) gv = __hip_atomic_load(gIn + 32 * (g + 1) + l32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const int Qo = Q;
+        Q = lo ? inV : Q;
+        if (g >= 3) emit(g - 3, Qo);
+        if (dbgOn) tWait += __builtin_amdgcn_s_memtime() - tw0;
+      };
+      for (int c = 0; c < NC; ++c) {
+        if (dbgOn && c == 1 && lane == 0) A.dbg[gw * 8 + 2] = __builtin_amdgcn_s_memrealtime();
+        if (rowInLds) {
+          C.codeLane = sRow + c * BG_CHUNK - lane - 1;
+        } else if (rowPacked) {
+          stage_packed(c);
+        } else {
+          stage_codes(c, cv);
+          fetch_codes(c + 1 < NC ? c + 1 : c, cv);
+        }
+        // the checkpoint stores go first: a boundary's own stores are then the youngest memory
+        // operations when the compute starts, and nothing waits on them before the next boundary
+        int32_t* ck = ckBase + (size_t)c * (R + 1) * BG_WAVE;
+#pragma unroll
+        for (int k = 0; k < R; ++k) ck[k * BG_WAVE] = S.Y[k];
+        ck[R * BG_WAVE] = S.topPrev;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        boundary(2 * c);
+        auto mid = [&]() { boundary(2 * c + 1); };
+        const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
+        if (edge) score_chunk_conv<R, TV_EDGE>(S, C, c, Q, mid);
+        else score_chunk_conv<R, TV_FAST>(S, C, c, Q, mid);
+      }
+      if (nh >= 1) emit(nh - 1, Q);                              // the last half: 2 NC - 3
+    } else {
+    // the last strip of a CONV-mode pair reads whole blocks of 64 granules, one block ahead
+    unsigned long long gL = 0;
+    if (CONVMODE && hbmAhead && 0 < nblk) gL = __hip_atomic_load(gIn + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // WIDE, strip above on another workgroup: its blocks come through HBM one chunk ahead of
     // use — block c + 1 (and the producer's counter for the check at chunk c + 1) is loaded
     // while chunk c computes, so neither the counter poll nor the block load (each a cross-XCD
@@ -244,12 +382,8 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     // compare consumes it).  The signal fences keep the compiler from moving the block load
     // above the poll; an agent acquire fence (vmcnt(0) + buffer_inv sc1, ~1.7 us) per chunk
     // would cost more than the chunk.
-    const bool hbmAhead = WIDE && s > 0 && !mailIn;
-    const int pwH = (s - 1) % GW;
-    const int needBase = ((s - 1) / GW) * nblk;
-    const int32_t* bndAbove = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + lane;
     int nbV = 0, pollV = 0;
-    if (hbmAhead) {
+    if (hbmAhead && !CONVMODE) {
       int np0 = 0;
       if (0 < nblk)
         while ((int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < needBase + 1)
@@ -258,18 +392,13 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       nbV = load_agent(bndAbove);
       pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // WIDE strips that hand their row down (every one but the last) run the one-register
-    // conveyor step (score_chunk_conv): no per-step LDS read of the row above, no ring write
-    const bool conv = WIDE && CKPT && !lastStrip;
-    int Q = 0;
-    const bool dbgOn = A.dbg != nullptr && rho == 0 && pairIdx == 0 && gw < 4096;
-    unsigned long long tWait = 0, tStart = dbgOn ? __builtin_amdgcn_s_memrealtime() : 0;
-    const unsigned long long cStart = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
     for (int c = 0; c < NC; ++c) {
       if (dbgOn && c == 1 && lane == 0) A.dbg[gw * 8 + 2] = __builtin_amdgcn_s_memrealtime();
       const unsigned long long tw0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
       if (rowInLds) {
         C.codeLane = sRow + c * BG_CHUNK - lane - 1;
+      } else if (rowPacked) {
+        stage_packed(c);
       } else {
         // this chunk's codes into LDS, the next chunk's in flight
         stage_codes(c, cv);
@@ -277,20 +406,27 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       }
       // the row above, block c: row 0, the producer's LDS mailbox, or HBM
       const int seq = rho * NC + c;                              // block sequence number
+      const int hseq = rho * nh + 2 * c;                         // CONV mode: its first half
       const int jb = c * BG_CHUNK + lane;
       if (s == 0) {
         const int m0 = wadd(row0_M(mode, jb, a, b), -wmul(a, jb));          // M'(0, j)
-        if (conv) Q = m0;
-        else {
-          waveLds[lane] = CKPT ? m0 : 4 * m0 + 2;                           // (X form)
-          C.bIn = waveLds;
+        waveLds[lane] = CKPT ? m0 : 4 * m0 + 2;                             // (X form)
+        C.bIn = waveLds;
+      } else if (hbmAhead && CONVMODE) {
+        if (c < nblk) {
+          int np = 0;
+          while (!__all((uint32_t)(gL >> 32) == ep)) {
+            wide_poll_pause(np);
+            gL = __hip_atomic_load(gIn + (size_t)c * BG_CHUNK + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          }
         }
+        waveLds[lane] = (int)(uint32_t)gL;
+        C.bIn = waveLds;
+        if (c + 1 < nblk)
+          gL = __hip_atomic_load(gIn + (size_t)(c + 1) * BG_CHUNK + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       } else if (hbmAhead) {
-        if (conv) Q = nbV;                                                  // block c
-        else {
-          waveLds[lane] = nbV;
-          C.bIn = waveLds;
-        }
+        waveLds[lane] = nbV;
+        C.bIn = waveLds;
         if (c + 1 < NC) {
           if (c + 1 < nblk) {
             int np1 = 0;
@@ -305,7 +441,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         }
       } else {
         if (c < nblk) {
-          const int need = ((s - 1) / GW) * nblk + c + 1;
+          const int need = CONVMODE ? hseq + 2 : ((s - 1) / GW) * nblk + c + 1;
           const int pw = mailIn ? prevW : (s - 1) % GW;
           if (WIDE && !mailIn) {
             int np2 = 0;
@@ -317,12 +453,9 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
               poll_pause<WIDE>(np);
           }
         }
-        if (mailIn && conv) {
-          // the block goes into the conveyor register now: the slot is free for the producer
-          Q = prevMail[(seq % kMailSlots) * 64 + lane];
-          if (lane == 0) __hip_atomic_store(sCons + w, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if (mailIn) {
-          C.bIn = prevMail + (seq % kMailSlots) * 64;
+        if (mailIn) {
+          // CONV mode: halves hseq, hseq + 1 sit in adjacent half slots (hseq is even)
+          C.bIn = CONVMODE ? prevMail + (hseq % KH) * 32 : prevMail + (seq % kMailSlots) * 64;
         } else {
           __atomic_signal_fence(__ATOMIC_SEQ_CST);                          // after the poll
           waveLds[lane] = load_agent(A.bndM + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK + jb);
@@ -346,14 +479,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
 #pragma unroll
         for (int k = 0; k < R; ++k) ck[k * BG_WAVE] = S.Y[k];
         ck[R * BG_WAVE] = S.topPrev;
-        if (conv) {
-          if (edge) score_chunk_conv<R, TV_EDGE>(S, C, c, Q);
-          else score_chunk_conv<R, TV_FAST>(S, C, c, Q);
-          if (c >= 1) {                                            // Q = block c - 1, final
-            if (C.mail) C.mail[lane] = Q;
-            __hip_atomic_store(C.bndOut + (c - 1) * BG_CHUNK + lane, Q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          }
-        } else if (edge) score_chunk<R, TV_EDGE, WIDE>(S, C, c);
+        if (edge) score_chunk<R, TV_EDGE, WIDE>(S, C, c);
         else if (lastStrip && selRow) score_chunk<R, TV_SEL, WIDE>(S, C, c);
         else if (R <= 4 && s == 0) {
           // row 0 above: M'(0, j) for j >= 1 is linear (semiglobal / local / overlap: M = 0;
@@ -396,8 +522,9 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
           if (lane == 0) __hip_atomic_store(sProg + w, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
-      if (mailIn && !conv && lane == 0)   // release: this chunk's reads of the slot are done
-        __hip_atomic_store(sCons + w, seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (mailIn && lane == 0)   // release: this chunk's reads of the slot(s) are done
+        __hip_atomic_store(sCons + w, CONVMODE ? hseq + 2 : seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     }
     if (dbgOn && lane == 0) {
       A.dbg[gw * 8 + 0] = (unsigned long long)s;
