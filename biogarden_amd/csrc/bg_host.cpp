@@ -1283,9 +1283,10 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
       if (!d[8 * g + 1]) continue;
       // every wave of a small group, else waves 64k .. 64k+7 + the last
       if (nrec > 64 && g % 64 >= 8 && g + 1 < 4096 && d[8 * (g + 1) + 1]) continue;
-      std::fprintf(stderr, "  wave %4d strip %4llu start %8.1f c0done %8.1f end %8.1f us  waited %10.0f of %10.0f cycles\n", g,
+      std::fprintf(stderr, "  wave %4d strip %4llu start %8.1f c0done %8.1f end %8.1f us  waited %10.0f of %10.0f cycles  data %10.0f flow %10.0f\n", g,
                    d[8 * g], (d[8 * g + 1] - t0) * 0.01, (d[8 * g + 2] - t0) * 0.01,
-                   (d[8 * g + 3] - t0) * 0.01, (double)d[8 * g + 4], (double)d[8 * g + 5]);
+                   (d[8 * g + 3] - t0) * 0.01, (double)d[8 * g + 4], (double)d[8 * g + 5],
+                   (double)d[8 * g + 6], (double)d[8 * g + 7]);
     }
   }
   if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.p && np) {

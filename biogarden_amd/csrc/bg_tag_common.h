@@ -33,6 +33,30 @@ struct TagCtx {
   int top0, topStep;        // score_chunk<..., TOP0>: M'(0, t0) and its step along row 0
 };
 
+// Column n2 in the score-only steps: the lane at column n2 keeps its R values in chunk-local
+// registers (one v_cndmask per row in the steps t in [n2, n2 + 64)) and the lanes that reached it
+// in this chunk store them at the chunk's end; a divergent 1-lane store per step there cost the
+// strip's last chunks ~200 cycles a step, and in the WIDE chain every strip's tail adds to the
+// next one's start.
+template <int R>
+__device__ __forceinline__ void catch_lastcol(const int (&Y)[R], int (&L)[R], int t, int n2, int lane) {
+  if (t >= n2 && t - n2 < BG_WAVE && n2 > 0) {              // wave-uniform
+    const bool sel = lane == t - n2;
+#pragma unroll
+    for (int k = 0; k < R; ++k) L[k] = sel ? Y[k] : L[k];
+  }
+}
+template <int R>
+__device__ __forceinline__ void store_lastcol(const int (&L)[R], const TagCtx& C, int t0) {
+  const int tl = C.n2 + C.lane;                              // the step this lane was at column n2
+  if (C.n2 <= 0 || tl < t0 || tl >= t0 + BG_CHUNK) return;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = C.rowbase + k + 1;
+    if (i <= C.n1) C.lastcol[i] = wadd(L[k], wmul(C.a, i + C.n2));
+  }
+}
+
 // profile dwords per lane and code: R int8 bytes, padded to an aligned ds_read width
 template <int R>
 struct ProfW { static constexpr int v = R <= 4 ? 1 : (R <= 8 ? 2 : 4); };
@@ -184,6 +208,7 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
   constexpr int RW = ProfW<R>::v;
+  int Lc[R] = {};                                            // TV_EDGE: column n2
   // operand pipeline depth: the profile entries and row-above inputs of the next PF steps are in
   // flight while a step computes.  One step hides the LDS latency at several waves per SIMD; a
   // lone wave per SIMD (WIDE) issues a step in a few tens of cycles, so it runs 4 steps ahead
@@ -240,15 +265,7 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
           }
           S.Xlast = rst ? S.Y[R - 1] : S.Xlast;
         }
-        if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {    // column n2: M(i, n2)
-          if (lane == t - C.n2) {
-#pragma unroll
-            for (int k = 0; k < R; ++k) {
-              const int i = C.rowbase + k + 1;
-              if (i <= C.n1) C.lastcol[i] = wadd(S.Y[k], wmul(a, i + C.n2));
-            }
-          }
-        }
+        catch_lastcol<R>(S.Y, Lc, t, C.n2, lane);            // column n2: M(i, n2)
       }
       int out = S.Xlast;
       if constexpr (VAR != TV_FAST) {
@@ -271,6 +288,7 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
       C.ring[lane] = C.ring[64 + lane];
     }
   }
+  if constexpr (VAR == TV_EDGE) store_lastcol<R>(Lc, C, t0);
 }
 
 // v_mov_b32_dpp wave_shl:1 — lane r receives lane r+1; lane 63 keeps `old`.
@@ -296,6 +314,7 @@ __device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
   constexpr int RW = ProfW<R>::v;
+  int Lc[R] = {};                                            // TV_EDGE: column n2
   constexpr int PF = 4;
   int qCode[PF];
   ProfV<RW> qP[PF];
@@ -340,15 +359,7 @@ __device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C
           }
           S.Xlast = rst ? S.Y[R - 1] : S.Xlast;
         }
-        if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {    // column n2: M(i, n2)
-          if (lane == t - C.n2) {
-#pragma unroll
-            for (int k = 0; k < R; ++k) {
-              const int i = C.rowbase + k + 1;
-              if (i <= C.n1) C.lastcol[i] = wadd(S.Y[k], wmul(a, i + C.n2));
-            }
-          }
-        }
+        catch_lastcol<R>(S.Y, Lc, t, C.n2, lane);            // column n2: M(i, n2)
       }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -357,6 +368,7 @@ __device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  if constexpr (VAR == TV_EDGE) store_lastcol<R>(Lc, C, t0);
 }
 
 }  // namespace bgk

@@ -32,6 +32,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "bg_dev_util.h"
 #include "bg_tag_common.h"
 
@@ -61,6 +63,19 @@ constexpr int kTagStageU16 = 192;
 #define BG_MAIL_SLOTS 4
 #endif
 constexpr int kMailSlots = BG_MAIL_SLOTS;   // boundary blocks in flight between two waves of a workgroup
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+using rsrc_t = __amdgpu_buffer_rsrc_t;
+constexpr int kSC1 = 16;                     // buffer op cache policy: sc1 (agent-coherent)
+// a raw buffer descriptor over [p, p + bytes) built from wave-uniform (readfirstlane) words, so
+// that the buffer ops need no waterfall loop
+__device__ __forceinline__ rsrc_t uniform_rsrc(const void* p, unsigned bytes) {
+  const unsigned long long x = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)x);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(x >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), 0,
+                                           (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
 
 // Polling pauses.  WIDE runs one wave per SIMD: nothing else wants the issue slots, and every
 // poll's wake-up latency adds to the strip's pace whenever it has caught up with its producer
@@ -282,59 +297,106 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
     unsigned long long* gOut = A.gran + P.bnd_off + (size_t)s * NC * BG_CHUNK;
     const unsigned long long* gIn = A.gran + P.bnd_off + (size_t)(s - 1) * NC * BG_CHUNK;
     if (CONVMODE && !lastStrip) {
+      // one loop per (incoming, outgoing) kind, so that no register of one kind's loads is
+      // reused by another kind's code (the compiler then waits vmcnt(0) on every such reuse)
+      auto conv_loop = [&](auto inK, auto outK) {
+      constexpr int IN = decltype(inK)::value;                   // 0 row 0, 1 mailbox, 2 granules
+      constexpr bool MOUT = decltype(outK)::value;               // consumer in this workgroup
       const bool lo = lane < 32;
       const int l32 = lane & 31;
       const int hb = rho * nh;                                   // this round's half sequence base
-      unsigned long long gv = 0;
-      if (hbmAhead && 0 < nh) gv = __hip_atomic_load(gIn + l32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // Global memory through buffer descriptors (wave-uniform SGPRs) and lane offsets computed
+      // once: the compiler waits vmcnt before it overwrites ANY register a pending memory op reads
+      // (address or data), so per-boundary 64-bit addresses in temporaries made every boundary
+      // wait for its own stores.  The data registers of this boundary's stores are kept live
+      // (kv, kg, ckv) until the next boundary, by when the stores have completed.
+      const rsrc_t rCk = uniform_rsrc(ckBase - lane, NC * (R + 1) * BG_WAVE * 4);
+      const rsrc_t rBnd = uniform_rsrc(C.bndOut, NC * BG_CHUNK * 4);
+      const rsrc_t rGo = uniform_rsrc(gOut, NC * BG_CHUNK * 8);
+      const int vL4 = lane * 4, vH4 = l32 * 4, vH8 = l32 * 8;
+      const rsrc_t rGi = uniform_rsrc(s > 0 ? gIn : gOut, NC * BG_CHUNK * 8);
+      u32x2 gv = {0u, 0u};
+      if (IN == 2 && 0 < nh) gv = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, 0, kSC1);
+      int kv = 0;
+      u32x2 kg = {0u, 0u};
+      int ckv[R + 1];
+#pragma unroll
+      for (int k = 0; k <= R; ++k) ckv[k] = 0;
       int Q = 0;
+      unsigned long long tData = 0, tFlow = 0;                   // BG_DP_TIMING: spin cycles
+      // LDS words read a boundary ahead (their latency hides behind the half's compute; the
+      // words are monotonic, so a stale read only sends the wave down the polling path):
+      // pc = the producer's half count, pv = the half after this boundary's (valid when pc says
+      // so: the count is read before the data, in this wave's LDS order, and the producer wrote
+      // the data before the count), fc = the consumer's release count
+      int pc = -1, pv = 0, fc = -(1 << 30);
       // half og of this strip's last row, in lanes 32-63 of v: to the consumer and to bndOut
       auto emit = [&](int og, int v) {
         const int col = 32 * og + l32;
-        if (mailOut) {
+        if constexpr (MOUT) {
           const int sq = hb + og;
-          int np = 0;
-          while (__hip_atomic_load(sCons + w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < sq + 1 - KH)
-            wide_poll_pause(np);
+          if (fc < sq + 1 - KH) {
+            int np = 0;
+            const unsigned long long tf0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
+            while ((fc = __hip_atomic_load(sCons + w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < sq + 1 - KH)
+              wide_poll_pause(np);
+            if (dbgOn) tFlow += __builtin_amdgcn_s_memtime() - tf0;
+          }
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
           if (!lo) mailbox[(sq % KH) * 32 + l32] = v;
           __atomic_signal_fence(__ATOMIC_SEQ_CST);              // LDS: the counter after the data
           if (lane == 0) __hip_atomic_store(sProg + w, sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else if (!lo) {
-          __hip_atomic_store(gOut + col, ((unsigned long long)ep << 32) | (uint32_t)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          fc = __hip_atomic_load(sCons + w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          kg = u32x2{(unsigned)v, ep};
+          if (!lo) __builtin_amdgcn_raw_buffer_store_b64(kg, rGo, vH8, og * 256, kSC1);
         }
-        if (!lo) __hip_atomic_store(C.bndOut + col, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        kv = v;
+        if (!lo) __builtin_amdgcn_raw_buffer_store_b32(kv, rBnd, vH4, og * 128, 0);
+        (void)col;
       };
       // before half g: the row above's half g into lanes 0-31 (lane 0 reads it at the next step),
       // the finished half g - 3 (lanes 32-63) out
       auto boundary = [&](int g) {
+        // the previous boundary's store data stays allocated until here
+        asm volatile("" ::"v"(kv), "v"(kg.x), "v"(kg.y));
         const unsigned long long tw0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
         int inV;
-        if (s == 0) {
+        if constexpr (IN == 0) {
           const int j = 32 * g + l32;
           inV = wadd(row0_M(mode, j, a, b), -wmul(a, j));                    // M'(0, j)
           for (int z = 0; z < A.wide_pace; ++z) __builtin_amdgcn_s_sleep(1);
-        } else if (mailIn) {
+        } else if constexpr (IN == 1) {
           const int sq = hb + g;
-          if (g < nh) {
+          if (g < nh && pc < sq + 1) {
             int np = 0;
+            const unsigned long long td0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
             while (__hip_atomic_load(sProg + prevW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < sq + 1)
               wide_poll_pause(np);
+            if (dbgOn) tData += __builtin_amdgcn_s_memtime() - td0;
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            pv = prevMail[(sq % KH) * 32 + l32];
           }
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-          inV = prevMail[(sq % KH) * 32 + l32];
+          inV = pv;
           __atomic_signal_fence(__ATOMIC_SEQ_CST);              // LDS: the release after the read
           if (lane == 0) __hip_atomic_store(sCons + w, sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          pc = __hip_atomic_load(sProg + prevW, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
+          pv = prevMail[((sq + 1) % KH) * 32 + l32];
         } else {
           if (g < nh) {
             int np = 0;
-            while (!__all(!lo || (uint32_t)(gv >> 32) == ep)) {
+            const unsigned long long td0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
+            while (!__all(!lo || gv.y == ep)) {
               wide_poll_pause(np);
-              gv = __hip_atomic_load(gIn + 32 * g + l32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              gv = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, g * 256, kSC1);
             }
+            if (dbgOn) tData += __builtin_amdgcn_s_memtime() - td0;
           }
-          inV = (int)(uint32_t)gv;
-          if (g + 1 < nh) gv = __hip_atomic_load(gIn + 32 * (g + 1) + l32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          inV = (int)gv.x;
+          if (g + 1 < nh) gv = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, (g + 1) * 256, kSC1);
         }
         const int Qo = Q;
         Q = lo ? inV : Q;
@@ -353,18 +415,41 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         }
         // the checkpoint stores go first: a boundary's own stores are then the youngest memory
         // operations when the compute starts, and nothing waits on them before the next boundary
-        int32_t* ck = ckBase + (size_t)c * (R + 1) * BG_WAVE;
 #pragma unroll
-        for (int k = 0; k < R; ++k) ck[k * BG_WAVE] = S.Y[k];
-        ck[R * BG_WAVE] = S.topPrev;
+        for (int k = 0; k <= R; ++k) {
+          ckv[k] = k < R ? S.Y[k] : S.topPrev;
+          asm volatile("" : "+v"(ckv[k]));                    // a register of its own
+          __builtin_amdgcn_raw_buffer_store_b32(ckv[k], rCk, vL4, (c * (R + 1) + k) * BG_WAVE * 4, 0);
+        }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         boundary(2 * c);
-        auto mid = [&]() { boundary(2 * c + 1); };
+        auto mid = [&]() {
+#pragma unroll
+          for (int k = 0; k <= R; ++k) asm volatile("" ::"v"(ckv[k]));
+          boundary(2 * c + 1);
+        };
         const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
         if (edge) score_chunk_conv<R, TV_EDGE>(S, C, c, Q, mid);
         else score_chunk_conv<R, TV_FAST>(S, C, c, Q, mid);
       }
       if (nh >= 1) emit(nh - 1, Q);                              // the last half: 2 NC - 3
+      if (dbgOn && lane == 0) {
+        A.dbg[gw * 8 + 6] = tData;
+        A.dbg[gw * 8 + 7] = tFlow;
+      }
+      };
+      using I0 = std::integral_constant<int, 0>;
+      using I1 = std::integral_constant<int, 1>;
+      using I2 = std::integral_constant<int, 2>;
+      using BT = std::integral_constant<bool, true>;
+      using BF = std::integral_constant<bool, false>;
+      if (s == 0) {
+        if (mailOut) conv_loop(I0{}, BT{}); else conv_loop(I0{}, BF{});
+      } else if (mailIn) {
+        if (mailOut) conv_loop(I1{}, BT{}); else conv_loop(I1{}, BF{});
+      } else {
+        if (mailOut) conv_loop(I2{}, BT{}); else conv_loop(I2{}, BF{});
+      }
     } else {
     // the last strip of a CONV-mode pair reads whole blocks of 64 granules, one block ahead
     unsigned long long gL = 0;
