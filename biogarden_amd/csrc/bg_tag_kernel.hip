@@ -315,8 +315,11 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       const rsrc_t rGo = uniform_rsrc(gOut, NC * BG_CHUNK * 8);
       const int vL4 = lane * 4, vH4 = l32 * 4, vH8 = l32 * 8;
       const rsrc_t rGi = uniform_rsrc(s > 0 ? gIn : gOut, NC * BG_CHUNK * 8);
-      u32x2 gv = {0u, 0u};
-      if (IN == 2 && 0 < nh) gv = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, 0, kSC1);
+      // two halves in flight: even halves in gvA, odd halves in gvB (the two boundary call sites
+      // of a chunk), so a load has two halves' time to land and is never copied while pending
+      u32x2 gvA = {0u, 0u}, gvB = {0u, 0u};
+      if (IN == 2 && 0 < nh) gvA = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, 0, kSC1);
+      if (IN == 2 && 1 < nh) gvB = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, 256, kSC1);
       int kv = 0;
       u32x2 kg = {0u, 0u};
       int ckv[R + 1];
@@ -358,7 +361,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       };
       // before half g: the row above's half g into lanes 0-31 (lane 0 reads it at the next step),
       // the finished half g - 3 (lanes 32-63) out
-      auto boundary = [&](int g) {
+      auto boundary = [&](int g, u32x2& gv) {
         // the previous boundary's store data stays allocated until here
         asm volatile("" ::"v"(kv), "v"(kg.x), "v"(kg.y));
         const unsigned long long tw0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
@@ -396,7 +399,7 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
             if (dbgOn) tData += __builtin_amdgcn_s_memtime() - td0;
           }
           inV = (int)gv.x;
-          if (g + 1 < nh) gv = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, (g + 1) * 256, kSC1);
+          if (g + 2 < nh) gv = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, (g + 2) * 256, kSC1);
         }
         const int Qo = Q;
         Q = lo ? inV : Q;
@@ -422,11 +425,11 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
           __builtin_amdgcn_raw_buffer_store_b32(ckv[k], rCk, vL4, (c * (R + 1) + k) * BG_WAVE * 4, 0);
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        boundary(2 * c);
+        boundary(2 * c, gvA);
         auto mid = [&]() {
 #pragma unroll
           for (int k = 0; k <= R; ++k) asm volatile("" ::"v"(ckv[k]));
-          boundary(2 * c + 1);
+          boundary(2 * c + 1, gvB);
         };
         const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
         if (edge) score_chunk_conv<R, TV_EDGE>(S, C, c, Q, mid);
