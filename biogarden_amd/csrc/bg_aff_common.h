@@ -117,6 +117,7 @@ __device__ __forceinline__ void aff_chunk(AffStrip<R, LOCAL>& S, const AffCtx& C
   const int t0 = c * BG_CHUNK;
   const int lane = C.lane;
   constexpr int RW = AffW<R>::v;
+  int Lc[R] = {};                           // TV_EDGE, non-local: M at column n2 (see below)
   int2 nTop = C.bIn[0];
   ProfV<RW> nP = load_prof<RW>(C.profLane + C.codeLane[0]);
   int nCode = C.codeLane[1];
@@ -174,14 +175,13 @@ __device__ __forceinline__ void aff_chunk(AffStrip<R, LOCAL>& S, const AffCtx& C
           oX = rst ? kAffNeg : oX;
         }
         if constexpr (!LOCAL) {
-          if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {  // column n2: M(i, n2)
-            if (lane == t - C.n2) {
+          // column n2: M(i, n2), caught in registers by the lane passing it and stored at the
+          // chunk's end (a divergent one-lane store per step made these chunks ~200 cycles a
+          // step slower, bg_tag_common.h catch_lastcol)
+          if (t >= C.n2 && t - C.n2 < BG_WAVE && C.n2 > 0) {  // wave-uniform
+            const bool sel = lane == t - C.n2;
 #pragma unroll
-              for (int k = 0; k < R; ++k) {
-                const int i = C.rowbase + k + 1;
-                if (i <= C.n1) C.lastcol[i] = wadd(wadd(S.M[k], -oc), wmul(C.b, i + C.n2));
-              }
-            }
+            for (int k = 0; k < R; ++k) Lc[k] = sel ? S.M[k] : Lc[k];
           }
         }
       }
@@ -204,6 +204,16 @@ __device__ __forceinline__ void aff_chunk(AffStrip<R, LOCAL>& S, const AffCtx& C
       C.ring[lane] = nx;
     } else if (h == 1) {
       C.ring[lane] = C.ring[64 + lane];
+    }
+  }
+  if constexpr (VAR == TV_EDGE && !LOCAL) {
+    const int tl = C.n2 + lane;                   // the step this lane was at column n2
+    if (C.n2 > 0 && tl >= t0 && tl < t0 + BG_CHUNK) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int i = C.rowbase + k + 1;
+        if (i <= C.n1) C.lastcol[i] = wadd(wadd(Lc[k], -oc), wmul(C.b, i + C.n2));
+      }
     }
   }
 }
