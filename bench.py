@@ -322,7 +322,9 @@ def kernel_info(st, pipeline):
             "pipeline": pipeline, "fin_waves": st["fin_waves"], "fin_slots": st["fin_slots"]}
 
 
-CONFIG_STEPS = {"C2": 12, "C3": 12, "C4": 12, "C5": 8}
+# K for the configs legs: the metric's default (20) for every configuration, so that each leg's
+# last traceback (outside any overlap, inside the timed region) weighs the same 1/K in all of them
+CONFIG_STEPS = {"C2": 20, "C3": 20, "C4": 20, "C5": 20}
 
 
 def config_leg(h, sc, name, barrier, pipeline, steps=None):
