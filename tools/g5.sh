@@ -7,3 +7,4 @@ for d in 3 4; do
   timeout -k 10 200 python tools/configs.py C3 --steps 12 --pipeline $d > gpurun_out/c3_5_d$d.txt 2>&1 || exit 4
   tail -1 gpurun_out/c3_5_d$d.txt
 done
+BG_DP_TIMING=800 timeout -k 10 120 python tools/dp_timeline.py --pairs 1 --len 100000 > gpurun_out/tl_c3_5_ch800.txt 2>&1 || exit 5
