@@ -280,8 +280,7 @@ extern "C" bg_aligner* bg_aligner_new(int device) {
     h->cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream4, hipStreamNonBlocking) != hipSuccess) {
+      hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess) {
     bg_aligner_free(h);
     return nullptr;
   }
@@ -345,7 +344,7 @@ extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
   if (!h || depth < 1 || depth > 4) return BG_E_ARG;
   if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream2) != hipSuccess || hipStreamSynchronize(h->stream3) != hipSuccess ||
-      hipStreamSynchronize(h->stream4) != hipSuccess)
+      (h->stream4 && hipStreamSynchronize(h->stream4) != hipSuccess))
     return BG_E_HIP;
   h->depth = depth;
   h->prepared = false;   // arenas are sized at prepare time
@@ -678,7 +677,7 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
-  BG_HIP(hipStreamSynchronize(h->stream4));
+  if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
   tm.mark(kPhSync, "sync");
   for (Slot& S : h->slot) S.inflight = false;
   h->execCount = 0;
@@ -1161,6 +1160,13 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   if ((h->wide || std::getenv("BG_TWO_FIN_STREAMS")) && !std::getenv("BG_FINISH_TIMING") &&
       !std::getenv("BG_ONE_FIN_STREAM"))
     nfs = h->wide ? std::min(3, std::max(2, h->depth - 1)) : 2;
+  // the third stream is created on first use: HIP maps a process's streams onto 4 hardware
+  // queues round-robin, and an extra stream per handle moves other handles' copies behind
+  // kernels in a shared queue (host_to_host runs four handles)
+  if (nfs == 3 && !h->stream4 && hipStreamCreateWithFlags(&h->stream4, hipStreamNonBlocking) != hipSuccess) {
+    h->stream4 = nullptr;
+    nfs = 2;
+  }
   const hipStream_t fss[3] = {h->stream2, h->stream3, h->stream4};
   hipStream_t fs = fss[h->execCount % nfs];
   BG_HIP(hipStreamWaitEvent(fs, S.dpDone, 0));
@@ -1249,7 +1255,7 @@ extern "C" int bg_synchronize(bg_aligner* h) {
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
-  BG_HIP(hipStreamSynchronize(h->stream4));
+  if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
   if (h->executed) {
     (void)hipEventElapsedTime(&h->dp_ms, h->last[0], h->last[1]);
     (void)hipEventElapsedTime(&h->fin_ms, h->last[2], h->last[3]);
@@ -1448,7 +1454,7 @@ extern "C" int bg_profile_end(bg_aligner* h, float* avg_dp, float* avg_fin, int*
   BG_HIP(hipStreamSynchronize(h->stream));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
-  BG_HIP(hipStreamSynchronize(h->stream4));
+  if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
   double dp = 0, fin = 0;
   const int cnt = h->ringUsed / 4;
   for (int i = 0; i < cnt; ++i) {
@@ -1475,7 +1481,7 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   BG_HIP(hipSetDevice(h->device));
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
-  BG_HIP(hipStreamSynchronize(h->stream4));
+  if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
   const Slot& S = h->slot[h->lastSlot];
   const uint64_t n = h->npairs;
   BG_HIP(hipMemcpyAsync(dst, &n, 8, hipMemcpyHostToDevice, h->stream));
@@ -1522,7 +1528,7 @@ extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) 
     E.dst = nullptr;
     BG_HIP(hipStreamSynchronize(h->stream2));
     BG_HIP(hipStreamSynchronize(h->stream3));
-    BG_HIP(hipStreamSynchronize(h->stream4));
+    if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
     BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), h->stream));
     const unsigned g = (unsigned)(((uint64_t)E.nplan + 255) / 256);
     if (g) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(g), dim3(256), args, 0, h->stream));
