@@ -50,9 +50,11 @@ sys.path.insert(0, ROOT)
 # the host_to_host leg runs four handles of three streams each, and with four queues a handle's
 # string download waits in a queue behind another handle's DP kernel (fetch D2H 1.7-2.1 ms per
 # batch against 0.41 ms with a queue per stream; tools/g12.sh).  Read by HIP at its
-# initialisation, so set before torch or the library loads; the value `value` is measured at is
-# unaffected (one handle, three streams).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# initialisation, so set before torch or the library loads (raised to 16, never lowered; the
+# environment may already name HIP's default 4); `value` is unaffected (one handle, three
+# streams).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 from tools import workloads  # noqa: E402
 
