@@ -47,13 +47,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (default 4) round-robin;
-# the host_to_host leg runs four handles of three streams each, and with four queues a handle's
-# string download waits in a queue behind another handle's DP kernel (fetch D2H 1.7-2.1 ms per
-# batch against 0.41 ms with a queue per stream; tools/g12.sh).  Read by HIP at its
-# initialisation, so set before torch or the library loads (raised to 16, never lowered; the
-# environment may already name HIP's default 4); `value` is unaffected (one handle, three
-# streams).
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+# with fewer queues than the host_to_host leg's streams, a handle's string download waits in a
+# queue behind another handle's DP kernel (fetch D2H 1.7-2.1 ms per batch against 0.41 ms with a
+# queue per stream; profiles/r03/h2h_queues/).  Read by HIP at its initialisation: a value the
+# environment sets is kept (and the leg sizes its handle rotation to it, host_to_host.hw_queues);
+# only when unset does the bench ask for 16.
+HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
+if not HW_QUEUES_ENV:
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 from tools import workloads  # noqa: E402
@@ -394,7 +394,9 @@ def main():
     ap.add_argument("--no-affine", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host timing")
-    ap.add_argument("--h2h-handles", type=int, default=4)
+    ap.add_argument("--h2h-handles", type=int, default=0,
+                    help="handles in the host-to-host rotation (0: 4 when the process has >= 12 "
+                         "hardware queues, else 2)")
     ap.add_argument("--h2h-rounds", type=int, default=24,
                     help="timed batches of the host-to-host leg (the stream's fill and drain, "
                          "~one batch's latency, spread over them)")
@@ -534,9 +536,12 @@ def main():
     # ---- host-to-host rate (not `value`): host buffers in, aligned strings back on the host
     h2h = None
     if not args.no_h2h:
+        queues = int(os.environ.get("GPU_MAX_HW_QUEUES") or 4)
+        nh = args.h2h_handles or (4 if queues >= 12 else 2)
         h2h = host_to_host(pairs, args.mode, args.open, args.extend, local_rank,
-                           pipeline=args.pipeline, handles=args.h2h_handles,
-                           rounds=args.h2h_rounds)
+                           pipeline=args.pipeline, handles=nh, rounds=args.h2h_rounds)
+        h2h["hw_queues"] = queues
+        h2h["hw_queues_source"] = "environment" if HW_QUEUES_ENV else "bench default (unset)"
 
     if rank != 0:
         h.close()

@@ -669,8 +669,10 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
                         const HScore& S, int32_t a, int32_t b) {
   if (!h || mode < BG_GLOBAL || mode > BG_SEMIGLOBAL || S.K < 1 || S.K > 256) return BG_E_ARG;
   if (npairs && (!s1 || !n1 || !s2 || !n2)) return BG_E_ARG;
-  std::vector<std::pair<long, long>> callDims;   // consumed by this prepare (aligner calls only)
-  if (!h->finFlags) callDims.swap(h->callDims);
+  // the pending per-pair dims (aligner calls only): copied, and consumed only when this prepare
+  // succeeds, so a prepare that fails early (argument, HIP or memory error) leaves them for a retry
+  std::vector<std::pair<long, long>> callDims;
+  if (!h->finFlags) callDims = h->callDims;
   PhaseTimer tm(h->hostMs);
   ++h->nPrepare;
   BG_HIP(hipSetDevice(h->device));
@@ -1058,6 +1060,7 @@ plan_again:
   h->bufCols = bufC;
   fin_geom(h, h->plan.size(), &h->finWaves, &h->finSlots);
   tm.mark(kPhPlan, "fin_geom");
+  if (!h->finFlags) h->callDims.clear();
   h->prepared = true;
   return BG_OK;
 }

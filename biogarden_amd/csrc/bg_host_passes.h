@@ -299,8 +299,9 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
   if (!rec || bytes < 32 || (np && (!res || !n1 || !n2 || !s1 || !s2))) return BG_E_ARG;
   uint64_t head[4];
   std::memcpy(head, rec, 32);
-  if (head[0] != 0x31434742ull || head[1] != np) return BG_E_ARG;
+  if (head[0] != 0x31434742ull || head[1] != np || head[3] > 4) return BG_E_ARG;
   const uint64_t opsBytes = head[2];
+  const bool semi = head[3] == 4;                      // bg_mode of the batch (BG_SEMIGLOBAL)
   if (bytes < 32 + np * sizeof(bg_compact_hdr) + opsBytes) return BG_E_ARG;
   const uint8_t* ops = rec + 32 + np * sizeof(bg_compact_hdr);
   std::vector<bg_compact_hdr> hd(np);
@@ -324,9 +325,19 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
       c2 += op != 1;
     }
     if (h.start1 + c1 != h.end_i || h.start2 + c2 != h.end_j) return BG_E_ARG;
+    // the reference's semiglobal assembly (aligner.rs:389-428): the tail gap columns run from the
+    // end cell to the last row / column, and a walk that returned (status 0) is preceded by the
+    // prefix of the sequence it stopped in, exactly up to its start cell (row case: s2[0, start2),
+    // column case: s1[0, start1)); the other modes have neither
     const bool colcase = h.end_i < n1[p];
-    if (h.npre && (colcase ? h.npre > n1[p] : h.npre > n2[p])) return BG_E_ARG;
-    if (h.ntail && (colcase ? h.end_i + h.ntail > n1[p] : h.end_j + h.ntail > n2[p])) return BG_E_ARG;
+    if (!semi) {
+      if (h.npre || h.ntail) return BG_E_ARG;
+    } else {
+      const uint64_t tail = colcase ? n1[p] - h.end_i : n2[p] - h.end_j;
+      const uint64_t pre = colcase ? h.start1 : h.start2;
+      if (h.status == 0 ? (h.npre != pre || h.ntail != tail) : (h.npre != 0 || (h.ntail && h.ntail != tail)))
+        return BG_E_ARG;
+    }
   }
   par_ranges(np, [&](size_t p) -> uint64_t { return 2ull * hd[p].len + 64; }, [&](size_t lo, size_t hi) {
     for (size_t p = lo; p < hi; ++p) {

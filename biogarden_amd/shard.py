@@ -106,6 +106,11 @@ def gather_packed(local, dist, dst=0):
         if sz[rank]:
             for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), dst)]):
                 w.wait()
+            # with RCCL, wait() only orders torch's current stream: block the host until the send
+            # has read `local`, so the caller may overwrite it (the next step's export runs on the
+            # library's own stream, which is not ordered after this one)
+            if dev.type == "cuda":
+                torch.cuda.current_stream(dev).synchronize()
         return None
     bufs = [None] * world
     ops = []

@@ -169,6 +169,8 @@ int main() {
   for (int it = 0; it < 60; ++it) {
     setenv("BG_HOST_THREADS", threads[it % 3], 1);
     const size_t np = rng() % 30;
+    const uint64_t mode = (it % 3 == 0) ? (uint64_t)(rng() % 4) : 4;   // mostly semiglobal
+    const bool semi = mode == 4;
     std::vector<std::string> a(np), b(np), w1(np), w2(np);
     std::vector<bg_compact_hdr> hd(np);
     std::vector<uint8_t> ops;
@@ -196,10 +198,11 @@ int main() {
       }
       h.start1 = (uint32_t)s1; h.start2 = (uint32_t)s2; h.end_i = (uint32_t)i; h.end_j = (uint32_t)j;
       const bool colcase = i < n1;
-      h.npre = (uint32_t)(rng() % 2 ? 0 : (colcase ? (n1 ? rng() % (n1 + 1) : 0) : (n2 ? rng() % (n2 + 1) : 0)));
-      h.ntail = (uint32_t)(rng() % 2 ? 0 : (colcase ? rng() % (n1 - i + 1) : rng() % (n2 - j + 1)));
+      // semiglobal assembly (aligner.rs:389-428): the tail runs to the last row / column; a
+      // returned walk (status 0) has the prefix up to its start cell; other modes have neither
+      h.npre = (uint32_t)(semi && h.status == 0 ? (colcase ? s1 : s2) : 0);
+      h.ntail = (uint32_t)(semi && (h.status == 0 || rng() % 2) ? (colcase ? n1 - i : n2 - j) : 0);
       h.len = (uint32_t)(h.npre + core.size() + h.ntail);
-      if (h.len > n1 + n2) { h.npre = 0; h.ntail = 0; h.len = (uint32_t)core.size(); }
       h.ops_off = ops.size();
       for (size_t q = 0; q < core.size(); q += 4) {
         uint8_t v = 0;
@@ -220,7 +223,7 @@ int main() {
       hd[p] = h;
     }
     std::vector<uint8_t> rec(32 + np * sizeof(bg_compact_hdr) + ops.size());
-    const uint64_t head[4] = {0x31434742ull, np, ops.size(), 4};
+    const uint64_t head[4] = {0x31434742ull, np, ops.size(), mode};
     std::memcpy(rec.data(), head, 32);
     if (np) std::memcpy(rec.data() + 32, hd.data(), np * sizeof(bg_compact_hdr));
     if (!ops.empty()) std::memcpy(rec.data() + 32 + np * sizeof(bg_compact_hdr), ops.data(), ops.size());
@@ -256,6 +259,26 @@ int main() {
       std::memcpy(&h0, bad.data() + 32, sizeof(h0));
       h0.end_i += 1;                                   // consumption no longer matches
       std::memcpy(bad.data() + 32, &h0, sizeof(h0));
+      CHECK(bgh::compact_expand(bad.data(), bad.size(), np, p1.data(), n1.data(), p2.data(), n2.data(),
+                                res.data(), o1.data(), o2.data(), cap) == BG_E_ARG);
+      // a prefix / tail inconsistent with the start / end cells (or present outside semiglobal)
+      for (int kind = 0; kind < 2; ++kind) {
+        bad = rec;
+        std::memcpy(&h0, bad.data() + 32, sizeof(h0));
+        if (kind == 0) {
+          if (!semi || h0.status != 0) { h0.npre += 1; }
+          else { h0.npre = h0.npre ? h0.npre - 1 : 1; }
+        } else {
+          const bool cc0 = h0.end_i < n1[0];
+          h0.ntail = (uint32_t)((cc0 ? n1[0] - h0.end_i : n2[0] - h0.end_j) + 1);   // past the end
+        }
+        h0.len = h0.npre + h0.ntail + (hd[0].len - hd[0].npre - hd[0].ntail);
+        std::memcpy(bad.data() + 32, &h0, sizeof(h0));
+        CHECK(bgh::compact_expand(bad.data(), bad.size(), np, p1.data(), n1.data(), p2.data(), n2.data(),
+                                  res.data(), o1.data(), o2.data(), cap) == BG_E_ARG);
+      }
+      bad = rec;
+      reinterpret_cast<uint64_t*>(bad.data())[3] = 7;  // no such mode
       CHECK(bgh::compact_expand(bad.data(), bad.size(), np, p1.data(), n1.data(), p2.data(), n2.data(),
                                 res.data(), o1.data(), o2.data(), cap) == BG_E_ARG);
     }
