@@ -154,12 +154,22 @@ def kernel_name(st):
     return "bg_dp_kernel<R=%d>" % st["R"]
 
 
-def roofline(st, cells, dp_ms, workload, a, b):
+def finish_name(st):
+    if st.get("split"):
+        return "split traceback (bg_exit_kernel<R=%d> + bg_finish_kernel phases)" % st["R"]
+    return "bg_finish_kernel<R=%d,%s>" % (st["R"], "checkpoint" if st["checkpoint"] else "trace")
+
+
+def roofline(st, cells, dp_ms, workload, a, b, fin_ms=None):
     """§8(d): algorithmic bytes per cell 0.25 (open >= extend: 2-bit m_trace) or 0.5 (4-bit trace)
-    plus the residues, over the DP kernel's event-timed launch; VALU from the PMC summary."""
+    plus the residues, over the event-timed launch of the step's DOMINANT kernel: the DP, or the
+    traceback stream when it runs longer (its kernels' time on their stream); VALU from the PMC
+    summary (the DP's)."""
     bpc = 0.25 if a >= b else 0.5
     algo = cells * bpc + st["residue_bytes"]
-    achieved = algo / (dp_ms * 1e-3) / 1e9 if dp_ms > 0 else 0.0
+    fin_dom = fin_ms is not None and fin_ms > dp_ms
+    dom_ms = fin_ms if fin_dom else dp_ms
+    achieved = algo / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     pmc = load_pmc(workload)
     same = pmc.get("geometry") == [str(st["R"]), str(st["waves"])]
     traffic = pmc.get("hbm_bytes_per_launch") if same else None
@@ -176,12 +186,14 @@ def roofline(st, cells, dp_ms, workload, a, b):
                      "frac_of_measured_issue": round(ipc * cps / MEASURED_ISSUE_LANE_OPS, 4),
                      "pmc_source": "profiles/pmc_%s.json" % workload})
     return {"bound": "valu", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "frac_basis": "HBM roofline of SURVEY 8(d): (%.2f B/cell + residues) / DP kernel time "
-                          "/ 8 TB/s; the binding roof is VALU issue (see valu.frac)" % bpc,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic if not fin_dom else None,
+            "frac_basis": "HBM roofline of SURVEY 8(d): (%.2f B/cell + residues) / the dominant "
+                          "kernel's time / 8 TB/s; the binding roof is VALU issue (see valu.frac)" % bpc,
             "algorithmic_bytes_per_launch": int(algo),
-            "traffic_source": ("profiles/pmc_%s.json" % workload) if traffic else None,
-            "kernel": kernel_name(st), "kernel_ms": round(dp_ms, 4), "valu": valu}
+            "traffic_source": ("profiles/pmc_%s.json" % workload) if (traffic and not fin_dom) else None,
+            "kernel": finish_name(st) if fin_dom else kernel_name(st),
+            "kernel_ms": round(dom_ms, 4), "dominant": "traceback" if fin_dom else "dp",
+            "dp_kernel": kernel_name(st), "dp_ms": round(dp_ms, 4), "valu": valu}
 
 
 # ------------------------------------------------------------------ timed runs
@@ -327,7 +339,8 @@ def cpu_section(pairs, gpu_scores, mode, a, b, info, pairs_multi, pairs_one):
 
 def kernel_info(st, pipeline):
     return {"R": st["R"], "waves": st["waves"], "affine": st["affine"], "tagged": st["tagged"],
-            "checkpoint": st["checkpoint"], "wide": st["wide"], "dna_profile": st["dna"],
+            "checkpoint": st["checkpoint"], "wide": st["wide"], "split": st.get("split", 0),
+            "dna_profile": st["dna"],
             "pipeline": pipeline, "fin_waves": st["fin_waves"], "fin_slots": st["fin_slots"]}
 
 
@@ -352,14 +365,35 @@ def config_leg(h, sc, name, barrier, pipeline, steps=None):
     k = steps or CONFIG_STEPS[name]
     el, dp, fin = timed(h, k, 2, barrier)
     res = h.fetch_raw()
-    roof = roofline(st, st["cells"], dp, name, a, b)
+    roof = roofline(st, st["cells"], dp, name, a, b, fin)
     roof["finish_ms"] = round(fin, 4)
+    single = None
+    if name == "C3":
+        # SURVEY 8(d)'s wall of ONE alignment: execute + synchronize, nothing in flight before it
+        walls, dps, fins = [], [], []
+        for _ in range(5):
+            h.synchronize()
+            t0 = time.perf_counter()
+            h.execute()
+            h.synchronize()
+            walls.append((time.perf_counter() - t0) * 1e3)
+            s2 = h.stats()
+            dps.append(s2["dp_ms"])
+            fins.append(s2["finish_ms"])
+        med = sorted(walls)[len(walls) // 2]
+        single = {"wall_ms": round(med, 4), "wall_ms_min": round(min(walls), 4),
+                  "dp_ms": round(sorted(dps)[2], 4), "traceback_ms": round(sorted(fins)[2], 4),
+                  "value": round(st["cells"] / (med * 1e-3) / 1e9, 3), "unit": "GCUPS", "runs": 5,
+                  "covers": "one bg_batch_execute (DP, end cell, traceback, strings) + synchronize, "
+                            "median of 5"}
+        if st.get("split"):
+            single["split_stats"] = h.split_stats()
     return {"workload": workloads.DESCRIPTION[name], "pairs": len(pairs), "cells": st["cells"],
             "share": share, "value": round(st["cells"] * k / el / 1e9, 3), "unit": "GCUPS",
             "steps": k, "ms_per_step": round(el / k * 1e3, 4), "dp_ms": round(dp, 4),
             "finish_ms": round(fin, 4), "kernel": kernel_info(st, pipeline), "roofline": roof,
             "all_status_ok": all(x in (0, 4) for x in res["status"]),
-            "status4": sum(1 for x in res["status"] if x == 4)}
+            "status4": sum(1 for x in res["status"] if x == 4), "single": single}
 
 
 def main():
@@ -486,7 +520,7 @@ def main():
     else:
         heads0 = [_native.compact_headers(b) for b in gatherer(h, None, coll_dev, gstats)()]
     workload = workload_name(args.mode, args.pairs, args.len1, args.len2, args.open, args.extend)
-    roof = roofline(st, cells, dp_ms, workload, args.open, args.extend)
+    roof = roofline(st, cells, dp_ms, workload, args.open, args.extend, fin_ms)
     roof["finish_ms"] = round(fin_ms, 4)
 
     # ---- strong scaling beside the weak headline (N > 1): one batch of 256 pairs over the ranks
@@ -519,7 +553,7 @@ def main():
         ea = max_over_ranks(ea)
         resa = h.fetch_raw()
         wla = workload_name(args.mode, args.pairs, args.len1, args.len2, a2, b2)
-        ra = roofline(sta, sta["cells"], dpa, wla, a2, b2)
+        ra = roofline(sta, sta["cells"], dpa, wla, a2, b2, fina)
         ra["finish_ms"] = round(fina, 4)
         aff = {"workload": wla, "value": round(sum_over_ranks(sta["cells"]) * na / ea / 1e9, 3),
                "unit": "GCUPS", "steps": na, "ms_per_step": round(ea / na * 1e3, 4),
@@ -616,7 +650,7 @@ def job_line(args, h, sc, world, rank, dist, coll_dev, barrier, max_over_ranks, 
     el2, _, _ = timed(h, steps, 1, barrier)
     el2 = max_over_ranks(el2)
     packed = g()
-    roof = roofline(st, st["cells"], dp, name, a, b)
+    roof = roofline(st, st["cells"], dp, name, a, b, fin)
     roof["finish_ms"] = round(fin, 4)
     if rank == 0:
         from biogarden_amd import shard

@@ -25,7 +25,7 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_aligner_set_call_dims", "bg_host_timing", "bg_last_hip_error",
            "bg_batch_export_compact", "bg_compact_expand", "bg_fasta_open",
            "bg_batch_prepare_table", "bg_fasta_next_batch",
-           "bg_fasta_close"]
+           "bg_fasta_close", "bg_split_stats"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -65,7 +65,8 @@ class BgStats(ctypes.Structure):
                 ("wide", ctypes.c_int32), ("workgroups", ctypes.c_int32),
                 ("checkpoint", ctypes.c_int32),
                 ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float),
-                ("fin_waves", ctypes.c_int32), ("fin_slots", ctypes.c_int32)]
+                ("fin_waves", ctypes.c_int32), ("fin_slots", ctypes.c_int32),
+                ("split", ctypes.c_int32)]
 
 
 class BgFastaBatch(ctypes.Structure):
@@ -114,6 +115,7 @@ def lib():
     L.bg_batch_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
                                  ctypes.c_size_t]
     L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
+    L.bg_split_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 4
     L.bg_aligner_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.c_size_t)]
     L.bg_aligner_set_buffer_size.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t]
@@ -394,6 +396,14 @@ class Handle:
         st = BgStats()
         check(lib().bg_get_stats(self._p, ctypes.byref(st)))
         return {f: getattr(st, f) for f, _ in BgStats._fields_}
+
+    def split_stats(self):
+        """bg_split_stats: the last execute's split traceback (pairs split, strips stitched,
+        moves the stitching walked itself, pairs whose exit pass overflowed)."""
+        v = [ctypes.c_uint64() for _ in range(4)]
+        check(lib().bg_split_stats(self._p, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("pairs_split", "strips_taken", "tail_moves", "pairs_overflow"),
+                        (x.value for x in v)))
 
 
 def expand_compact(rec, pairs):

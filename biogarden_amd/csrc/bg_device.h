@@ -34,6 +34,72 @@ struct BgPair {
   int32_t buf_rows;    // the reference aligner's scratch when this pair's call starts (rows, cols)
   int32_t buf_cols;
   uint64_t ops_off;    // byte offset of this pair's packed core ops (ceil((n1+n2)/4) bytes)
+  uint64_t split_off;  // split traceback (bg_split.hip): int32 offset of the pair's split area
+};
+
+// ---- split traceback (WIDE linear checkpoint batches).  The walk of one long
+// pair is cut at strip boundaries: an exit pass gives every cell of a strip's bottom row the
+// column where its traceback path enters the strip above (its "exit"), a chain over the strips
+// turns the start cell into one entry column per strip, and the strips' walks then run as
+// independent workgroups that the tail stitches together.
+#define BG_SPLIT_EBITS 17                          // exit column field of the packed values
+#define BG_SPLIT_SYM(R) ((1 << BG_SPLIT_EBITS) - ((R) + 1) * 64)   // first symbolic exit
+#define BG_SPLIT_SEGC 16                           // default chunks per exit-pass segment
+
+// Per (pair, strip) record of a strip walk.
+struct BgStripHdr {
+  int32_t sk, sl;      // cell the walk started from
+  int32_t ek, el;      // cell it stopped at (crossed: the first cell in the strip above)
+  int32_t nops;        // ops written to the strip's scratch (backwards from its end)
+  int32_t crossed;     // 1: stopped on entering the strip above; 0: the walk ended in this strip
+  int32_t status;      // 0, 4 (reference index underflow), 5 (internal)
+  int32_t pre;         // tail: ops of the strips stitched before this one
+};
+
+// Split area of one pair (int32 offsets from BgPair::split_off; `ops` is a byte offset from the
+// area's start).  head: [0] end row, [1] end column, [2] score, [3] column case, [4] raw exit of
+// the start cell, [5] its segment, [6] overflow flag, [7] start strip (-1: nothing to split).
+struct BgSplitLayout {
+  uint64_t head, startcol, hdr, ebot, front, fres, ops, total_ints;
+  int32_t G, F, capS;
+};
+__host__ __device__ inline BgSplitLayout bg_split_layout(int n1, int n2, int nstrips, int nc, int R,
+                                                         int segc) {
+  BgSplitLayout L;
+  const uint64_t S = (uint64_t)nstrips;
+  L.G = (nc + segc - 1) / segc;
+  L.F = (R + 1) * 64;
+  L.capS = 64 * R + n2 + 1;
+  (void)n1;
+  uint64_t o = 0;
+  L.head = o; o += 16;
+  L.startcol = o; o += (S + 15) / 16 * 16;
+  L.hdr = o; o += S * 8;
+  L.ebot = o; o += (S * (uint64_t)(n2 + 1) + 15) / 16 * 16;
+  L.front = o; o += S * (uint64_t)L.G * L.F;
+  L.fres = o; o += S * (uint64_t)L.G * L.F;
+  L.ops = o * 4;
+  o += (S * (uint64_t)L.capS + 63) / 64 * 16;
+  L.total_ints = o;
+  return L;
+}
+
+// Exit pass, resolve and chain kernels (bg_split.hip).
+struct BgSplitArgs {
+  const BgPair* pairs;
+  const uint8_t* codes1;
+  const uint8_t* codes2;
+  const int32_t* ckpt;     // the slot's checkpoint arena (int32 view of the trace arena)
+  const int32_t* bndM;     // strip-boundary rows M'(last row of strip, j)
+  const int32_t* profile;  // [192 + q]: 4 packed int8 S(q, c) - 2a
+  int32_t* split;          // the slot's split arena
+  const int32_t* itemBase; // exit pass: first work item of each plan pair (npairs + 1)
+  const int32_t* stripBase;// resolve: first workgroup (strips 1 .. nstrips - 1) of each plan pair
+  int32_t npairs, nitems;
+  int32_t open, ext, mode, R, segc;
+  int32_t margin;          // headroom below a chunk's smallest input: clampv + max(0, max S - 2a) + 1
+  int32_t clampv;          // max(0, -(min S - 2a)): field value of a clamped column-0 value
+  int32_t grow;            // 65 * max(0, max S - 2a): growth of a value inside one chunk
 };
 
 // Would the reference SequenceAligner, whose scratch is rows x cols when this call starts
@@ -144,6 +210,20 @@ struct BgFinishArgs {
   int32_t nslots;          // checkpoint modes: recomputed-chunk slots in use (0: all)
   int32_t pstride;         // row stride of the int16 profile table (affine checkpoint path)
   uint8_t* ops;            // packed core ops (2 bits per column, op 0 diagonal, 1 up, 2 left)
+  // split traceback (linear checkpoint kernel only): BG_PH_* phase, the slot's split arena, the
+  // exit pass's segment length and, for BG_PH_WALK, the (plan index, strip) of each workgroup
+  int32_t phase;
+  int32_t segc;
+  int32_t* split;
+  const int2* splitMap;
+};
+
+// BgFinishArgs::phase
+enum {
+  BG_PH_FULL = 0,   // end cell + the whole walk + strings (one workgroup per pair)
+  BG_PH_HEAD = 1,   // end cell only, into the split head
+  BG_PH_WALK = 2,   // one strip's walk per workgroup, into the strip's scratch
+  BG_PH_TAIL = 3    // stitch the strip walks (finish any walk the chain did not cover) + strings
 };
 
 // BgFinishArgs::flags

@@ -83,6 +83,8 @@ __device__ __forceinline__ int unbias(unsigned v) { return (int)(v ^ 0x80000000u
 // staged in LDS, plus an 8x8 neighbourhood of decoded cells held one per lane.
 constexpr int kWinBytesMax = 57344;  // 56 KiB window + scalars/scan, under the 64 KiB default
 constexpr int kCodeMiss = 32, kCodeBorder = 16;
+// split traceback (BG_PH_WALK): a cell in the strip above the walked strip ends the strip's walk
+constexpr int kCodeSplit = 64;
 
 // ------------------------------------------------------------------ checkpoint traceback
 // One wave recomputes chunk c of strip s of a pair from the forward pass's checkpoint with the
@@ -284,8 +286,24 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     __syncthreads();
   }
 
-  const BgPair& P = F.pairs[blockIdx.x];
+  // split traceback phases (linear checkpoint traceback only, BgFinishArgs::phase): WALK runs one
+  // strip of a pair per workgroup (F.splitMap), the others one pair per workgroup
+  const int ph = LIN_CK ? F.phase : (int)BG_PH_FULL;
+  int pidx = (int)blockIdx.x, wstrip = -1;
+  if (ph == BG_PH_WALK) {
+    const int2 m = F.splitMap[blockIdx.x];
+    pidx = m.x;
+    wstrip = m.y;
+  }
+  const BgPair& P = F.pairs[pidx];
   const int tid = threadIdx.x, lane = tid & 63, wid = uni(tid >> 6), NT = blockDim.x;
+  int32_t* spl = nullptr;                              // the pair's split area
+  BgSplitLayout SL{};
+  if (ph != BG_PH_FULL) {
+    SL = bg_split_layout(P.n1, P.n2, P.nstrips, P.nc, R, F.segc);
+    spl = F.split + P.split_off;
+    if (ph == BG_PH_WALK && spl[SL.startcol + wstrip] < 0) return;   // the chain did not reach it
+  }
   Fin f;
   f.F = &F; f.P = &P;
   f.n1 = P.n1; f.n2 = P.n2; f.a = F.open; f.b = F.ext; f.mode = F.mode;
@@ -302,8 +320,13 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   // ---------------- end cell (aligner.rs:112, 173-176, 247-251, 308-312, 369-389): every
   // thread folds a strided share into 64-bit keys (value, then the index rule), the waves'
   // keys meet in LDS.  Keys: row/column folds `>= last` and `> first` become max of
-  // (bias(v) << 32 | j) and (bias(v) << 32 | ~i).
-  {
+  // (bias(v) << 32 | j) and (bias(v) << 32 | ~i).  The split phases after HEAD read it back.
+  if (ph != BG_PH_FULL && ph != BG_PH_HEAD) {
+    if (tid == 0) {
+      sh[0] = spl[SL.head + 0]; sh[1] = spl[SL.head + 1]; sh[2] = spl[SL.head + 2];
+      sh[3] = spl[SL.head + 3]; sh[9] = 0;
+    }
+  } else {
     u64 ka = 0, kb = 0;
     const int32_t* rowbest = f.lastcol + (n1 + 1);
     if (mode == BGK_LOCAL) {
@@ -367,6 +390,15 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   __syncthreads();
   const int ei = uni(sh[0]), score = uni(sh[2]), colcase = uni(sh[3]);
   int ej = uni(sh[1]);
+  if (ph == BG_PH_HEAD) {
+    // the split head: end cell, score, column case; the start strip for the exit pass and chain
+    if (tid == 0) {
+      spl[SL.head + 0] = ei; spl[SL.head + 1] = ej; spl[SL.head + 2] = score; spl[SL.head + 3] = colcase;
+      spl[SL.head + 4] = -1; spl[SL.head + 5] = 0; spl[SL.head + 6] = 0;
+      spl[SL.head + 7] = (P.nstrips > 0 && ei >= 1 && ej >= 1) ? (ei - 1) / ROWS : -1;
+    }
+    return;
+  }
 
   // ---------------- semiglobal tail gaps (:389-404): the last ntail columns of the slot; the
   // walk's op codes (0 = (s1, s2), 1 = (s1, '-'), 2 = ('-', s2)) go backwards in front of them
@@ -378,6 +410,20 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   const int stripBlocks = P.nc * (BG_CHUNK / BG_TRACE_BLK);
   int k = ei, l = ej, state = 0, status = 0, ncore = 0;
   int curS = -1, curB0 = 0, curNb = 0;
+  // where the walk's ops go (backwards from capw, after ntw columns): the pair's slot, or (WALK)
+  // the strip's scratch; a WALK stops at the first cell of the strip above (splitTop)
+  uint8_t* obw = ob;
+  int capw = cap, ntw = ntail, splitTop = 0, crossed = 0;
+  if (ph == BG_PH_WALK) {
+    const int sStar = spl[SL.head + 7];
+    k = (wstrip == sStar) ? ei : (wstrip + 1) * ROWS;
+    l = spl[SL.startcol + wstrip];
+    splitTop = wstrip * ROWS;
+    obw = reinterpret_cast<uint8_t*>(spl) + SL.ops + (size_t)wstrip * SL.capS;
+    capw = SL.capS;
+    ntw = 0;
+  }
+  const int kStart = k, lStart = l;
   int k0 = -1000000, l0 = -1000000;                  // neighbourhood anchor (invalid)
   int codes = 0;
   // Transition table of backtrack (aligner.rs:520-586), per state, indexed by the 4-bit cell code
@@ -416,6 +462,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   unsigned usedE = 0;
   auto decode_cell = [&](int kk, int ll) -> int {
     usedIdx = -1;
+    if (splitTop > 0 && kk <= splitTop) return kCodeSplit;             // the strip above (WALK)
     if (kk <= 0 || ll <= 0) return kCodeBorder | ((kk == 0) ? 2 : 1);  // column 0 'X', row 0 'Y'
     const int vr = kk - 1;
     const int sidx = vr / ROWS, rem = vr - sidx * ROWS, r = rem / R, q = rem - r * R;
@@ -538,6 +585,87 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       if (status) { k = 0; l = 0; }
     }
   }
+  // ---- split traceback, TAIL: stitch the strip walks.  Strip s* (the start cell's) was walked from
+  // the start cell, every strip s < s* the chain reached from the cell in its bottom row where the
+  // path enters it.  Going up from s*, a strip's walk is taken while it started exactly where the
+  // walk below it crossed into it; its ops are copied into the slot in walk order.  The first walk
+  // that ended inside its strip ends the traceback; if the chain broke before (an exit-pass
+  // overflow, or any inconsistency), the walker below continues from the last crossing, so the
+  // result never depends on the exit pass.
+  bool preDone = false;
+  int ffOps = 0;                                       // ops stitched from the strip walks
+  if (ph == BG_PH_TAIL) {
+    const int sStar = spl[SL.head + 7];
+    const int* scol = spl + SL.startcol;
+    const BgStripHdr* hd = reinterpret_cast<const BgStripHdr*>(spl + SL.hdr);
+    int* preArr = scan + 512;                         // LDS: the window holds no trace yet
+    const bool fits = sStar >= 0 && sStar + 1 + 512 <= F.win_bytes / 4;
+    if (tid == 0) { sh[12] = -1; sh[13] = -1; }
+    __syncthreads();
+    if (fits) {
+      for (int s = tid; s <= sStar; s += NT) {
+        bool ok = scol[s] >= 0;
+        int cr = 1;
+        if (ok) {
+          const BgStripHdr h = hd[s];
+          if (s == sStar) {
+            ok = h.sk == ei && h.sl == ej;
+          } else {
+            const BgStripHdr u = hd[s + 1];
+            ok = scol[s + 1] >= 0 && u.crossed && h.sk == u.ek && h.sl == u.el;
+          }
+          ok = ok && h.status != 5 && h.nops >= 0 && h.nops < SL.capS;
+          cr = h.crossed;
+        }
+        if (!ok) atomicMax(&sh[12], s);
+        else if (!cr) atomicMax(&sh[13], s);
+      }
+    }
+    __syncthreads();
+    const int sb = fits ? sh[12] : sStar, sd = sh[13];
+    // taken strips [lim, sStar]; fin: the walk ended in strip lim
+    const bool fin = sd > sb;
+    const int lim = fin ? sd : sb + 1;
+    const int nt = (fits && lim <= sStar) ? sStar - lim + 1 : 0;
+    if (nt > 0) {
+      // ops before strip s in walk order: the strips above it in [s, sStar] (reversed index
+      // x = sStar - s), one contiguous range per thread, then a scan of the thread sums
+      const int per = (nt + NT - 1) / NT;
+      const int x0 = tid * per < nt ? tid * per : nt, x1 = x0 + per < nt ? x0 + per : nt;
+      int sum = 0;
+      for (int x = x0; x < x1; ++x) sum += hd[sStar - x].nops;
+      scan[tid] = sum;
+      __syncthreads();
+      for (int o = 1; o < NT; o <<= 1) {
+        const int v = tid >= o ? scan[tid - o] : 0;
+        __syncthreads();
+        scan[tid] += v;
+        __syncthreads();
+      }
+      int acc = scan[tid] - sum;
+      for (int x = x0; x < x1; ++x) { preArr[x] = acc; acc += hd[sStar - x].nops; }
+      const int total = scan[NT - 1];
+      __syncthreads();
+      // copy: one wave per strip; the strip's ops sit at the end of its scratch in the slot's order
+      const uint8_t* scr = reinterpret_cast<const uint8_t*>(spl) + SL.ops;
+      for (int x = wid; x < nt; x += NWV) {
+        const int s = sStar - x;
+        const int n = hd[s].nops;
+        const uint8_t* src = scr + (size_t)s * SL.capS + (SL.capS - n);
+        uint8_t* dst = ob + (cap - ntail - preArr[x] - n);
+        for (int y = lane; y < n; y += 64) dst[y] = src[y];
+      }
+      ncore = total;
+      ffOps = total;
+      const BgStripHdr hl = hd[lim];
+      k = hl.ek;
+      l = hl.el;
+      if (fin) { status = hl.status; preDone = true; }
+      __threadfence_block();
+      __syncthreads();
+    }
+    if (tid == 0) { spl[SL.head + 8] = nt; spl[SL.head + 9] = preDone ? 1 : 0; }   // bg_split_stats
+  }
   u64 tJump = 0, tMiss = 0, nJump = 0, nMiss = 0, nRec = 0;   // BG_FINISH_TIMING instrumentation
   u64 nSelf = 0;                                            // chunks the walker recomputed itself
   int lastReqS = -1, lastReqB = -1, sameReq = 0;            // barrier path: repeated requests
@@ -556,7 +684,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   asyncPos = async;
   if (async) {
     if (tid == 0) {
-      sh[32] = 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0; sh[37] = 0; sh[56] = -1;
+      sh[32] = preDone ? 1 : 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0; sh[37] = 0; sh[56] = -1;
       for (int z = 0; z < 8; ++z) { sh[40 + z] = -1; sh[48 + z] = 0; }
     }
     __syncthreads();
@@ -588,7 +716,9 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         const int lOut = lw - (dkIn >= 16 ? (int)((long)remw * dlIn / dkIn) : remw);
         const int cExit = lOut >> 6;                       // this strip's chunk at its top row
         const int xE = (lOut + 62) >> 6;                   // the strip above's entry chunk
-        auto mk = [&](int ss, int cc) { return (ss < 0 || ss >= NSp || cc < 0 || cc >= NCp) ? -1 : (ss << 16) | cc; };
+        auto mk = [&](int ss, int cc) {
+          return (ss < 0 || ss >= NSp || cc < 0 || cc >= NCp || (wstrip > 0 && ss < wstrip)) ? -1 : (ss << 16) | cc;
+        };
         int cand[2 + 2 * kSpecDepth];
         constexpr int NCAND = 2 + 2 * kSpecDepth;
         cand[0] = req;
@@ -677,12 +807,12 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     }
   }
   for (;;) {
-    int reqS = -1, reqB0 = 0, done = 0;
+    int reqS = -1, reqB0 = 0, done = preDone ? 1 : 0;
     if (wid == 0) {
       // the walk is one latency-bound wave: first claim on the issue slots it shares with the
       // next execute's DP waves (two-stream pipeline)
       __builtin_amdgcn_s_setprio(3);
-      for (;;) {
+      for (; !preDone;) {
         int dk = k0 - k, dl = l0 - l;
         if ((unsigned)dk >= 8u || (unsigned)dl >= 8u) { reanchor(k, l); dk = 0; dl = 0; }
         int c = rdlane(codes, dk * 8 + dl);
@@ -691,12 +821,12 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           // without moving and the walk is a chain of m_trace moves.  Resolve the chain through
           // the whole neighbourhood at once by pointer jumping (4 rounds of ds_bpermute over the
           // 64 cells); the border, STOP and window-miss cells stay with the scalar walker below.
-          const bool jumpable = state == 0 && !(c & (kCodeMiss | kCodeBorder)) &&
+          const bool jumpable = state == 0 && !(c & (kCodeMiss | kCodeBorder | kCodeSplit)) &&
                                 (MODE != BGK_LOCAL || (c & 3) != 3);
           if (jumpable) {
             if ((dk | dl) != 0) { reanchor(k, l); c = rdlane(codes, 0); }
             const int cl = codes;
-            const bool term = (cl & (kCodeMiss | kCodeBorder)) || (MODE == BGK_LOCAL && (cl & 3) == 3);
+            const bool term = (cl & (kCodeMiss | kCodeBorder | kCodeSplit)) || (MODE == BGK_LOCAL && (cl & 3) == 3);
             const int mv = (int)(kLutM >> (4 * (cl & 15)) >> 2) & 3;   // 1 diag, 2 up, 3 left
             const int nk = (lane >> 3) + (mv != 3), nl = (lane & 7) + (mv != 2);
             const bool ex = !term && (nk >= 8 || nl >= 8);          // the move leaves the block
@@ -721,10 +851,10 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             const int exP = infoP & 1, mvP = infoP >> 1;
             const int nops = Dn + exP;
 #if BG_FIN_DEBUG
-            if (lane == 0 && ntail + ncore + nops > cap)
-              printf("BGDBG pair %d: jumper writes op %d of cap %d at (%d, %d)\n", P.index, ntail + ncore + nops, cap, k, l);
+            if (lane == 0 && ntw + ncore + nops > capw)
+              printf("BGDBG pair %d: jumper writes op %d of cap %d at (%d, %d)\n", P.index, ntw + ncore + nops, capw, k, l);
 #endif
-            if (lane < nops) ob[cap - 1 - (ntail + ncore + lane)] = (uint8_t)opx;
+            if (lane < nops) obw[capw - 1 - (ntw + ncore + lane)] = (uint8_t)opx;
             ncore += nops;
             k -= Pn >> 3;
             l -= Pn & 7;
@@ -746,16 +876,16 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           // found by one find-first-set over a 64-bit lane mask; the same for Y along the row.
           // What is left is a chain over the 64 M nodes with weights (ops per hop), resolved by
           // pointer jumping with one ds_bpermute per round; the ops are emitted in parallel.
-          const bool termC = (c & (kCodeMiss | kCodeBorder)) || (MODE == BGK_LOCAL && (c & 3) == 3);
+          const bool termC = (c & (kCodeMiss | kCodeBorder | kCodeSplit)) || (MODE == BGK_LOCAL && (c & 3) == 3);
           if (!termC) {
             if ((dk | dl) != 0) reanchor(k, l);
             const int cl = codes;
-            const bool tm = (cl & (kCodeMiss | kCodeBorder)) || (MODE == BGK_LOCAL && (cl & 3) == 3);
+            const bool tm = (cl & (kCodeMiss | kCodeBorder | kCodeSplit)) || (MODE == BGK_LOCAL && (cl & 3) == 3);
             const u64 Tm = ballot(tm);
             const u64 TX = Tm | ballot(cl & 4);        // a run up stops here (x_trace 'M' or end)
             const u64 TY = Tm | ballot(cl & 8);
             auto emit = [&](int pos, int n, int op) {  // ops pos .. pos+n-1 of this walk
-              for (int q = 0; q < n; ++q) ob[cap - 1 - (ntail + pos + q)] = (uint8_t)op;
+              for (int q = 0; q < n; ++q) obw[capw - 1 - (ntw + pos + q)] = (uint8_t)op;
             };
             // the run the walk is in at the anchor (state X / Y), resolved in scalar
             int s0 = 0;
@@ -825,6 +955,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             continue;
           }
         }
+        if (c & kCodeSplit) { crossed = 1; done = 1; break; }   // entered the strip above (WALK)
         if (c & kCodeMiss) {
           const int vr = k - 1;
           reqS = vr / ROWS;
@@ -955,19 +1086,19 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         const int mv = e >> 2;
         if ((mv == 2 && k == 0) || (mv == 3 && l == 0)) { status = 4; done = 1; break; }  // index underflow panic
 #if BG_FIN_DEBUG
-        if (lane == 0 && mv && ntail + ncore + 1 > cap)
-          printf("BGDBG pair %d: scalar walker writes op %d of cap %d at (%d, %d)\n", P.index, ntail + ncore + 1, cap, k, l);
+        if (lane == 0 && mv && ntw + ncore + 1 > capw)
+          printf("BGDBG pair %d: scalar walker writes op %d of cap %d at (%d, %d)\n", P.index, ntw + ncore + 1, capw, k, l);
 #endif
         k -= (0x6 >> mv) & 1;
         l -= (0xA >> mv) & 1;
         state = e & 3;
         if (mv) {
-          if (lane == 0) ob[cap - 1 - (ntail + ncore)] = (uint8_t)(mv - 1);
+          if (lane == 0) obw[capw - 1 - (ntw + ncore)] = (uint8_t)(mv - 1);
           ++ncore;
         }
       }
       __builtin_amdgcn_s_setprio(0);
-      if (lane == 0) { sh[4] = reqS; sh[5] = reqB0; sh[6] = done; }
+      if (lane == 0) { sh[4] = reqS; sh[5] = reqB0; sh[6] = done; sh[11] = crossed; }
       if (async && lane == 0) __hip_atomic_store(&sh[32], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __syncthreads();
@@ -1072,6 +1203,17 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   // ---------------- semiglobal prefix gaps (:416-428); every wave knows k, l through sh
   if (wid == 0 && lane == 0) { sh[7] = k; sh[8] = l; sh[10] = ncore; if (sh[9] != 5) sh[9] = status; }
   __syncthreads();
+  if (ph == BG_PH_TAIL && tid == 0) spl[SL.head + 10] = sh[10] - ffOps;   // moves the tail walked
+  if (ph == BG_PH_WALK) {
+    // the strip's record for the tail
+    if (tid == 0) {
+      BgStripHdr hr;
+      hr.sk = kStart; hr.sl = lStart; hr.ek = sh[7]; hr.el = sh[8]; hr.nops = sh[10];
+      hr.crossed = sh[11]; hr.status = sh[9]; hr.pre = 0;
+      reinterpret_cast<BgStripHdr*>(spl + SL.hdr)[wstrip] = hr;
+    }
+    return;
+  }
   const int kstop = sh[7], lstop = sh[8];
   status = sh[9];
   ncore = sh[10];

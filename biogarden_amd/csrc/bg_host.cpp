@@ -32,6 +32,8 @@ extern "C" void* bg_dp_kernel_p32_ptr(int R, int affine, int local, int global);
 extern "C" void* bg_dp_kernel_lcs_ptr(int R, int dna);
 extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt);
 extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode);
+extern "C" void* bg_split_kernel_ptr(int R, int which);
+extern "C" int bg_exit_lds_bytes(int R);
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
 extern "C" int bg_dp_tag_wave_lds_bytes(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
@@ -130,7 +132,7 @@ struct PhaseTimer {
 // Per-execute arenas.  Two slots let the finish kernel of execute k (stream2) run while the
 // DP kernel of execute k+1 (stream) fills the other slot's trace.
 struct Slot {
-  DevBuf trace, bndM, bndX, aux, out1, out2, results, ops, gran;
+  DevBuf trace, bndM, bndX, aux, out1, out2, results, ops, gran, split;
   hipEvent_t dpDone = nullptr, finDone = nullptr;
   bool inflight = false;
 };
@@ -185,6 +187,14 @@ struct bg_aligner {
   int codesInLds = 0;
   int auxLdsOff = 0;
   int wide = 0;                    // tagged kernel: pairs spread over groups of workgroups
+  // split traceback (bg_split.hip): WIDE linear checkpoint batches walk their pairs
+  // strip by strip in parallel; BG_SPLIT=0 walks them whole (one workgroup per pair)
+  int split = 0, segc = BG_SPLIT_SEGC, splitMargin = 0, splitClamp = 0, splitGrow = 0;
+  int splitItems = 0, splitResolve = 0;
+  uint64_t splitInts = 0;
+  std::vector<int2> splitMap;
+  std::vector<int32_t> splitBases;  // exit-pass item bases (np + 1), then resolve bases (np + 1)
+  DevBuf splitMapBuf, splitBaseBuf;
   int tagRow = 0;                  // tagged kernel: the code row staged whole in LDS
   std::vector<int> groupOf;        // caller pair -> workgroups (WIDE)
   std::vector<int2> wgmap;
@@ -221,7 +231,7 @@ struct bg_aligner {
                profScratch.cap;
     for (const Slot& S : slot)
       t += S.trace.cap + S.bndM.cap + S.bndX.cap + S.aux.cap + S.out1.cap + S.out2.cap + S.results.cap +
-           S.ops.cap + S.gran.cap;
+           S.ops.cap + S.gran.cap + S.split.cap;
     return t;
   }
 };
@@ -927,6 +937,52 @@ plan_again:
     h->cells += (uint64_t)n1[p] * n2[p];
     h->plan.push_back(P);
   }
+  // split traceback: WIDE linear checkpoint batches (few long pairs), exits within the packed
+  // field (n2 below the symbolic range), some pair with more than one strip
+  h->split = 0;
+  h->splitMap.clear();
+  h->splitBases.clear();
+  h->splitItems = h->splitResolve = 0;
+  h->splitInts = 0;
+  {
+    const char* ev = std::getenv("BG_SPLIT");
+    const char* es = std::getenv("BG_SPLIT_SEGC");
+    h->segc = es ? std::max(1, std::atoi(es)) : BG_SPLIT_SEGC;
+    bool ok = h->wide && h->ckpt && !h->affine && !h->finFlags && mode != BG_LOCAL && !(ev && ev[0] == '0');
+    bool multi = false;
+    for (const BgPair& P : h->plan) {
+      if (P.n2 + 1 >= BG_SPLIT_SYM(R)) ok = false;
+      if (P.nstrips >= 2) multi = true;
+    }
+    if (ok && multi) {
+      int dmin = 1 << 30, dmax = -(1 << 30);
+      for (int q = 0; q < KS; ++q)
+        for (int c = 0; c < KS; ++c)
+          if (present[q] && present[c]) {
+            const int d = S.at(q, c) - 2 * a;
+            dmin = std::min(dmin, d);
+            dmax = std::max(dmax, d);
+          }
+      h->splitClamp = std::max(0, -dmin);
+      h->splitMargin = h->splitClamp + std::max(0, dmax) + 1;
+      h->splitGrow = 65 * std::max(0, dmax);
+      h->split = 1;
+      const size_t np = h->plan.size();
+      h->splitBases.assign(2 * (np + 1), 0);
+      for (size_t q = 0; q < np; ++q) {
+        BgPair& P = h->plan[q];
+        const BgSplitLayout L = bg_split_layout(P.n1, P.n2, P.nstrips, P.nc, R, h->segc);
+        P.split_off = h->splitInts;
+        h->splitInts += (L.total_ints + 63) / 64 * 64;
+        const int ns1 = P.nstrips > 1 ? P.nstrips - 1 : 0;
+        h->splitBases[q + 1] = h->splitBases[q] + ns1 * L.G;
+        h->splitBases[np + 1 + q + 1] = h->splitBases[np + 1 + q] + ns1;
+        for (int s2 = 0; s2 < P.nstrips; ++s2) h->splitMap.push_back(make_int2((int)q, s2));
+      }
+      h->splitItems = h->splitBases[np];
+      h->splitResolve = h->splitBases[2 * np + 1];
+    }
+  }
   h->traceBytes = tro;
   h->opsBytes = po;
   h->compactExec = -1;
@@ -940,6 +996,8 @@ plan_again:
       !h->prof.ensure(std::max<size_t>(4096, (size_t)h->pstride * h->pstride * 4 + 64)) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
       !h->wgmapBuf.ensure(sizeof(int2) * (h->wgmap.size() + 1)) ||
       !h->gprogBuf.ensure(4 * ((size_t)h->progWords + 1)) ||
+      (h->split && (!h->splitMapBuf.ensure(sizeof(int2) * (h->splitMap.size() + 1)) ||
+                    !h->splitBaseBuf.ensure(4 * (h->splitBases.size() + 1)))) ||
       (h->pglob && !h->profScratch.ensure((h->plan.size() + 1) * (size_t)h->W * h->kdim * 64 * 4 * 4)))
     return BG_E_NOMEM;
   h->gridWgs = h->wide ? (int)h->wgmap.size() : (int)h->plan.size();
@@ -948,7 +1006,8 @@ plan_again:
     if (!S.trace.ensure(tro + 256) || !S.bndM.ensure(bo * 4 + 256) ||
         !S.bndX.ensure((h->affine || h->ack) ? bo * 4 + 256 : 256) || !S.aux.ensure(ao * 4 + 256) ||
         !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) || !S.ops.ensure(po + 16) ||
-        !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)))
+        !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)) ||
+        (h->split && !S.split.ensure(h->splitInts * 4 + 256)))
       return BG_E_NOMEM;
     // WIDE checkpoint batches hand strip rows between workgroups as epoch-tagged granules: a
     // fresh arena is zeroed so that no stale tag (of another handle) can match an epoch
@@ -1040,6 +1099,12 @@ plan_again:
                           hipMemcpyHostToDevice, h->stream));
   BG_HIP(hipMemcpyAsync(h->pairs.p, h->plan.data(), sizeof(BgPair) * h->plan.size(),
                           hipMemcpyHostToDevice, h->stream));
+  if (h->split) {
+    BG_HIP(hipMemcpyAsync(h->splitMapBuf.p, h->splitMap.data(), sizeof(int2) * h->splitMap.size(),
+                          hipMemcpyHostToDevice, h->stream));
+    BG_HIP(hipMemcpyAsync(h->splitBaseBuf.p, h->splitBases.data(), 4 * h->splitBases.size(),
+                          hipMemcpyHostToDevice, h->stream));
+  }
   {
     std::vector<BgPairResultDev> tmpl(npairs);
     for (size_t p = 0; p < npairs; ++p) {
@@ -1202,6 +1267,10 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.ops = S.ops.as<uint8_t>();
     F.area_ints = 0;
     F.flags = h->finFlags;
+    F.phase = BG_PH_FULL;
+    F.segc = h->segc;
+    F.split = S.split.as<int32_t>();
+    F.splitMap = h->splitMapBuf.as<int2>();
     if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;
     if (std::getenv("BG_FIN_SELFSERVE")) F.flags |= BG_FIN_SELFSERVE;
     if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(64 * (np + 1))) {
@@ -1231,7 +1300,45 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       F.win_bytes = win;
       void* ffn = bg_finish_ck_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
+      if (!h->split) {
+        BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
+      } else {
+        // split traceback: end cell -> exit pass -> per-strip resolve -> chain ->
+        // the strips' walks in parallel -> stitch + strings
+        BgSplitArgs X;
+        X.pairs = F.pairs;
+        X.codes1 = F.codes1;
+        X.codes2 = F.codes2;
+        X.ckpt = reinterpret_cast<const int32_t*>(F.trace);
+        X.bndM = F.bndM;
+        X.profile = F.profile;
+        X.split = F.split;
+        X.itemBase = h->splitBaseBuf.as<int32_t>();
+        X.stripBase = h->splitBaseBuf.as<int32_t>() + (np + 1);
+        X.npairs = (int32_t)np;
+        X.nitems = h->splitItems;
+        X.open = h->a;
+        X.ext = h->b;
+        X.mode = h->mode;
+        X.R = h->R;
+        X.segc = h->segc;
+        X.margin = h->splitMargin;
+        X.clampv = h->splitClamp;
+        X.grow = h->splitGrow;
+        void* xargs[] = {&X};
+        F.phase = BG_PH_HEAD;
+        BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
+        if (h->splitItems > 0)
+          BG_HIP(hipLaunchKernel(bg_split_kernel_ptr(h->R, 0), dim3((h->splitItems + 3) / 4), dim3(256), xargs,
+                                 bg_exit_lds_bytes(h->R), fs));
+        if (h->splitResolve > 0)
+          BG_HIP(hipLaunchKernel(bg_split_kernel_ptr(h->R, 1), dim3(h->splitResolve), dim3(256), xargs, 0, fs));
+        BG_HIP(hipLaunchKernel(bg_split_kernel_ptr(h->R, 2), dim3(np), dim3(64), xargs, 0, fs));
+        F.phase = BG_PH_WALK;
+        BG_HIP(hipLaunchKernel(ffn, dim3((unsigned)h->splitMap.size()), dim3(64 * fnw), args, lds, fs));
+        F.phase = BG_PH_TAIL;
+        BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
+      }
     } else {
       F.win_bytes = bg_finish_window_bytes(h->R, h->affine, np, h->cus);
       BG_HIP(hipLaunchKernel(bg_finish_kernel_ptr(h->R, h->affine, h->mode), dim3(np), dim3(256), args,
@@ -1410,6 +1517,26 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->finish_ms = h->fin_ms;
   o->fin_waves = h->finWaves;
   o->fin_slots = h->finSlots;
+  o->split = h->split;
+  return BG_OK;
+}
+
+extern "C" int bg_split_stats(bg_aligner* h, uint64_t* pairs_split, uint64_t* strips_taken,
+                              uint64_t* tail_moves, uint64_t* pairs_overflow) {
+  if (!h || !pairs_split || !strips_taken || !tail_moves || !pairs_overflow) return BG_E_ARG;
+  *pairs_split = *strips_taken = *tail_moves = *pairs_overflow = 0;
+  if (!h->split || !h->executed) return BG_OK;
+  const int rc = bg_synchronize(h);
+  if (rc) return rc;
+  const Slot& S = h->slot[h->lastSlot];
+  for (const BgPair& P : h->plan) {
+    int32_t head[16];
+    BG_HIP(hipMemcpy(head, S.split.as<int32_t>() + P.split_off, sizeof(head), hipMemcpyDeviceToHost));
+    if (head[6]) ++*pairs_overflow;
+    if (head[7] >= 0) ++*pairs_split;
+    if (head[7] >= 0 && head[8] > 0) *strips_taken += (uint64_t)head[8];
+    if (head[7] >= 0 && head[10] > 0) *tail_moves += (uint64_t)head[10];
+  }
   return BG_OK;
 }
 

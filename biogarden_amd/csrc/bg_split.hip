@@ -1,0 +1,457 @@
+// Split traceback for few long pairs (WIDE linear checkpoint batches, C3): the exit pass, the
+// per-strip resolve and the chain over the strips.  The walks themselves and
+// the stitching run in bg_finish_kernel's BG_PH_WALK / BG_PH_TAIL phases.
+//
+// The reference walks the traceback from the end cell one move at a time (backtrack,
+// src/alignment/aligner.rs:511-592; for open >= extend the X / Y states fall back to M at once,
+// so the walk is a chain of m_trace moves).  Every cell of the DP has exactly one predecessor,
+// so the path from a cell of strip s (rows s*64R+1 .. (s+1)*64R) enters the row above the strip
+// at one column: the cell's exit.  With every bottom-row cell's exit known, the start cell's
+// entry column into each strip above follows from one lookup per strip, and the strips' walks no
+// longer depend on each other.
+//
+// Exit pass.  Work items are (pair, strip, segment of SEGC chunks).  A wave restarts the strip's
+// forward recurrence at the segment's first checkpoint (the same data the checkpoint traceback
+// recomputes chunks from) and sweeps the segment with the tagged step of bg_tag_kernel.hip,
+// except that a value is packed as
+//     (M'(i,j) - base) << 19  |  tag << 17  |  exit
+// with tag 0 diagonal / 2 X form / 3 Y form as in the tagged kernel.  The predecessor choice is
+// the tag's (v_max3_u32 compares value first, then tag: the reference's Y > X > R priority,
+// aligner.rs:455-463), and the three candidates never tie on (value, tag), so the exit bits below
+// ride along with the winner for free: the step is the tagged kernel's four VALU operations per
+// cell.  `base` is wave-uniform, re-chosen at every chunk start from the chunk's inputs; if a
+// chunk's values could leave the 13-bit field the pass sets the pair's overflow flag and the
+// tail walks the pair sequentially (the reference semantics never depend on this pass).
+// Column 0 (and the never-read cells left of it) is left out of the base: in global mode the
+// border a + (i-1)b lies ~i below column 1 (interior gaps cost a, the border b per row), so deep
+// strips would overflow on it.  A column-0 value below the base is clamped to the field value
+// c = max(0, -(min S - 2a)), and the base keeps c + max(S - 2a) + 1 of headroom below every other
+// input, so a candidate derived from a clamped value (left, or diagonal + S - 2a, never below 0)
+// stays strictly below the column-1 cell's up candidate, which truly wins there too (M' never
+// decreases down a column).
+// Exits are columns of the row above (concrete), or, for paths that leave the segment through
+// its left edge, symbolic references to the segment's first frontier (the R values and the
+// top-left input of every lane at the segment start), resolved strip by strip afterwards.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bg_dev_util.h"
+#include "bg_device.h"
+
+using namespace bgk;
+
+namespace {
+
+constexpr int kEBits = BG_SPLIT_EBITS;
+constexpr unsigned kEMask = (1u << kEBits) - 1;
+constexpr unsigned kT1 = 1u << kEBits;       // one tag unit
+constexpr unsigned kT2 = 2u << kEBits;       // X form
+constexpr unsigned kT3 = 3u << kEBits;       // Y form
+constexpr int kVShift = kEBits + 2;
+constexpr int kVMax = (1 << (32 - kVShift)) - 1;
+
+template <int R>
+__host__ __device__ constexpr int exit_wave_ints() {
+  return 4 * R * 64 + 64 + 96;               // profile [code][k][lane], top block, 192 u16 codes
+}
+
+__device__ __forceinline__ unsigned umax3(unsigned x, unsigned y, unsigned z) {
+  return __builtin_elementwise_max(__builtin_elementwise_max(x, y), z);
+}
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// v_mov_b32_dpp wave_shl:1 — lane r receives lane r+1; lane 63 keeps `old`
+__device__ __forceinline__ unsigned dpp_shl1u(unsigned old, unsigned src) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)src, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ unsigned dpp_shr1u(unsigned old, unsigned src) {
+  return (unsigned)__builtin_amdgcn_update_dpp((int)old, (int)src, 0x138, 0xf, 0xf, false);
+}
+
+template <int R>
+struct ExitStrip {
+  unsigned Y[R];      // Y form of the lane's rows at the previous column
+  unsigned topPrev;   // X form of (row above the lane, j - 1)
+  unsigned Xlast;     // X form of the lane's last row: handed to lane r + 1 by the DPP
+  unsigned Q;         // bottom-row conveyor: lane 63's last row of the chunk's steps
+};
+
+// One chunk of the packed tagged step.  EDGE: chunk 0 (column 0 borders, aligner.rs:98-104);
+// CAP: the chunk holds the walk's start cell, whose exit is captured at step `ts`.
+template <int R, bool EDGE, bool CAP>
+__device__ __forceinline__ void exit_chunk(ExitStrip<R>& S, int c, int lane, const int* profLane,
+                                           const uint16_t* codeLane, const unsigned* bIn,
+                                           const unsigned* col0, int ts, int qs, int rs,
+                                           unsigned& cap) {
+  const int t0 = c * 64;
+  // operand pipeline: the profile entries of step u + 1 and the code of step u + 2 are in flight
+  // while step u computes
+  unsigned nTop = bIn[0];
+  unsigned nP[R];
+  {
+    const int o = codeLane[0];
+#pragma unroll
+    for (int k = 0; k < R; ++k) nP[k] = (unsigned)profLane[o + k * 64];
+  }
+  int nCode = codeLane[1];
+#pragma unroll
+  for (int u = 0; u < 64; ++u) {
+    const int t = t0 + u;
+    const unsigned topIn = nTop;
+    unsigned P[R];
+#pragma unroll
+    for (int k = 0; k < R; ++k) { P[k] = nP[k]; nP[k] = (unsigned)profLane[nCode + k * 64]; }
+    nCode = codeLane[u + 2];
+    if (u + 1 < 64) nTop = bIn[u + 1];
+    const unsigned topX = dpp_shr1u(topIn, S.Xlast);       // X form of (row above, j)
+    unsigned dIn = S.topPrev;                               // X form of (row above, j - 1)
+    unsigned xo = topX;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const unsigned yo = S.Y[k];
+      const unsigned d = dIn + P[k];                        // tag 0: (S - 2a) << 19 - tag of dIn
+      const unsigned best = umax3(d, xo, yo);
+      const unsigned yn = best | kT3;                       // Y form for column j + 1
+      dIn = yo;
+      xo = yn - kT1;                                        // X form for row i + 1
+      S.Y[k] = yn;
+    }
+    S.topPrev = topX;
+    S.Xlast = xo;
+    if constexpr (EDGE) {
+      if (c == 0 && t == lane) {                            // column 0: border, exit 0
+#pragma unroll
+        for (int k = 0; k < R; ++k) S.Y[k] = col0[k];
+        S.Xlast = col0[R - 1] - kT1;
+      }
+    }
+    S.Q = dpp_shl1u(S.Y[R - 1], S.Q);
+    if constexpr (CAP) {
+      if (t == ts) {
+        unsigned v = S.Y[0];
+#pragma unroll
+        for (int k = 1; k < R; ++k) v = (k == qs) ? S.Y[k] : v;
+        cap = (unsigned)__builtin_amdgcn_readlane((int)v, rs);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+}  // namespace
+
+// One wave per (pair, strip s >= 1, segment g).  Outputs (split area of the pair):
+//   ebot[s][j]        raw exit of the strip's bottom row at column j (strips s < start strip)
+//   front[s][g][x]    raw exits of the segment's last frontier, x = k * 64 + lane (k < R: the
+//                     lane's rows; k = R: its top-left input), for segment g + 1's symbols
+//   head[4], head[5]  raw exit of the walk's start cell and its segment (start strip only)
+//   head[6]           set when a chunk's values could leave the packed field
+template <int R>
+__global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
+  extern __shared__ __attribute__((aligned(16))) int esm[];
+  constexpr int ROWS = 64 * R;
+  constexpr int F = (R + 1) * 64;
+  constexpr unsigned kSym = BG_SPLIT_SYM(R);
+  const int lane = threadIdx.x & 63;
+  const int w = uni(threadIdx.x >> 6);
+  const int item = uni((int)blockIdx.x * 4 + w);
+  if (item >= A.nitems) return;
+  int p = 0;
+  while (p + 1 < A.npairs && A.itemBase[p + 1] <= item) ++p;
+  p = uni(p);
+  const BgPair P = A.pairs[p];
+  const int n1 = P.n1, n2 = P.n2, NC = P.nc, NS = P.nstrips;
+  const BgSplitLayout L = bg_split_layout(n1, n2, NS, NC, R, A.segc);
+  const int rel = item - A.itemBase[p];
+  const int s = 1 + rel / L.G, g = rel % L.G;
+  int32_t* ar = A.split + P.split_off;
+  const int sStar = uni(ar[L.head + 7]);
+  if (s > sStar || s >= NS) return;
+  const int c0 = g * A.segc;
+  const int c1 = min(NC, c0 + A.segc);
+  const int a = A.open, b = A.ext, mode = A.mode;
+
+  int* wl = esm + w * exit_wave_ints<R>();
+  int* prof = wl;                                       // [code][k][lane]
+  unsigned* bIn = reinterpret_cast<unsigned*>(wl + 4 * R * 64);
+  uint16_t* stage = reinterpret_cast<uint16_t*>(wl + 4 * R * 64 + 64);
+  const int rowbase = s * ROWS + lane * R;
+  const uint8_t* cr1 = A.codes1 + P.off1;
+  const uint8_t* cr2 = A.codes2 + P.off2;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = rowbase + k + 1;
+    const int q = (i <= n1) ? cr1[i - 1] : 0;
+    const int pk = A.profile[192 + (q >> 3)];
+    const unsigned tadj = (k == 0 ? 2u : 3u) << kEBits;  // the tag of the diagonal's form
+#pragma unroll
+    for (int cd = 0; cd < 4; ++cd) {
+      const int v = __builtin_amdgcn_sbfe(pk, 8 * cd, 8);   // S(q, cd) - 2a
+      prof[(cd * R + k) * 64 + lane] = (int)(((unsigned)v << kVShift) - tadj);
+    }
+  }
+  const int* profLane = prof + lane;
+  const uint16_t* codeLane = stage + 63 - lane;
+  // the start cell, when it lies in this strip (lane rs, row qs, step ts)
+  const int ei = ar[L.head + 0], ej = ar[L.head + 1];
+  const bool capStrip = (s == sStar) && ei >= 1 && ej >= 1;
+  const int vs = ei - 1 - s * ROWS;
+  const int rs = capStrip ? vs / R : 0, qs = capStrip ? vs % R : 0, ts = capStrip ? ej + rs : -1;
+  const int32_t* topRow = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * 64;   // M'(s*ROWS, j)
+  const int tclamp = n2 < NC * 64 - 1 ? n2 : NC * 64 - 1;
+  auto top_abs = [&](int c) { const int j = c * 64 + lane; return topRow[j <= tclamp ? j : tclamp]; };
+
+  // initial state: the segment's first checkpoint (absolute M'), or the strip start
+  int Yabs[R], tpAbs;
+  unsigned Ye[R], tpE;
+  if (c0 == 0) {
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      const int i = rowbase + k + 1;
+      Yabs[k] = wadd(col0_M(mode, i, a, b), -wmul(a, i));
+      Ye[k] = 0;
+    }
+    tpAbs = Yabs[0];                                     // never read by a valid cell
+    tpE = 0;
+  } else {
+    const int32_t* ck = A.ckpt + P.trace_off / 4 + ((size_t)(s * NC + c0) * (R + 1)) * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < R; ++k) { Yabs[k] = ck[k * 64]; Ye[k] = kSym + (unsigned)(k * 64 + lane); }
+    tpAbs = ck[R * 64];
+    tpE = lane == 0 ? (unsigned)(c0 * 64 - 1) : kSym + (unsigned)(R * 64 + lane);
+  }
+  int mt = top_abs(c0);
+  ExitStrip<R> S;
+  int base = 0;
+  // field value of an absolute M' (0 for a clamped column-0 value)
+  auto fld = [&](int x) { return (unsigned)max(x - base, A.clampv) << kVShift; };
+  {
+    // the lanes' frontier cells sit at column c0 * 64 - 1 - lane, the top block at c0 * 64 + lane
+    const bool inF = c0 * 64 - 1 - lane >= 1, inT = c0 * 64 + lane >= 1;
+    int lo = inT ? mt : 0x7fffffff, hi = inT ? mt : -0x7fffffff - 1;
+    if (inF) {
+      lo = min(lo, tpAbs); hi = max(hi, tpAbs);
+#pragma unroll
+      for (int k = 0; k < R; ++k) { lo = min(lo, Yabs[k]); hi = max(hi, Yabs[k]); }
+    }
+    lo = uni(wave_min(lo));
+    hi = uni(wave_max(hi));
+    base = lo - A.margin;
+    if ((long)hi - base + A.grow > kVMax) { if (lane == 0) ar[L.head + 6] = 1; return; }
+#pragma unroll
+    for (int k = 0; k < R; ++k) S.Y[k] = fld(Yabs[k]) | kT3 | Ye[k];
+    S.topPrev = fld(tpAbs) | kT2 | tpE;
+    S.Xlast = S.Y[R - 1] - kT1;
+    S.Q = 0;
+  }
+  unsigned col0[R];
+  unsigned cap = 0xFFFFFFFFu;
+  int32_t* ebot = ar + L.ebot + (size_t)s * (n2 + 1);
+  const bool wantBot = s < sStar;
+  for (int c = c0; c < c1; ++c) {
+    if (c > c0) {
+      // re-base on this chunk's inputs: the lanes' values, their top-left inputs, the top block
+      // (column 0 left out: only chunk 1's lane 63 holds it)
+      const bool inF = c * 64 - 1 - lane >= 1;
+      int lo = mt - base, hi = mt - base;
+      if (inF) {
+        lo = min(lo, (int)(S.topPrev >> kVShift)); hi = max(hi, (int)(S.topPrev >> kVShift));
+#pragma unroll
+        for (int k = 0; k < R; ++k) { lo = min(lo, (int)(S.Y[k] >> kVShift)); hi = max(hi, (int)(S.Y[k] >> kVShift)); }
+      }
+      lo = uni(wave_min(lo));
+      hi = uni(wave_max(hi));
+      const int d = lo - A.margin;                       // new base - old base
+      if ((long)hi - d + A.grow > kVMax) { if (lane == 0) ar[L.head + 6] = 1; return; }
+      auto reb = [&](unsigned v) {
+        return ((unsigned)max((int)(v >> kVShift) - d, A.clampv) << kVShift) | (v & ((1u << kVShift) - 1));
+      };
+#pragma unroll
+      for (int k = 0; k < R; ++k) S.Y[k] = reb(S.Y[k]);
+      S.topPrev = reb(S.topPrev);
+      S.Xlast = reb(S.Xlast);
+      base += d;
+    }
+    bIn[lane] = fld(mt) | kT2 | (unsigned)(c * 64 + lane);
+    if (c + 1 < c1) mt = top_abs(c + 1);                 // in flight while the chunk computes
+#pragma unroll
+    for (int qq = 0; qq < 3; ++qq) {
+      const int x = c * 64 - 64 + lane + 64 * qq;
+      const int v = ((unsigned)x < (unsigned)n2) ? cr2[x] >> 3 : 0;
+      stage[lane + 64 * qq] = (uint16_t)(v * R * 64);
+    }
+    if (c == 0) {
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int i = rowbase + k + 1;
+        col0[k] = fld(wadd(col0_M(mode, i, a, b), -wmul(a, i))) | kT3;
+      }
+    }
+    const bool capHere = ts >= c * 64 && ts < c * 64 + 64;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    if (c == 0) {
+      if (capHere) exit_chunk<R, true, true>(S, c, lane, profLane, codeLane, bIn, col0, ts, qs, rs, cap);
+      else exit_chunk<R, true, false>(S, c, lane, profLane, codeLane, bIn, col0, ts, qs, rs, cap);
+    } else {
+      if (capHere) exit_chunk<R, false, true>(S, c, lane, profLane, codeLane, bIn, col0, ts, qs, rs, cap);
+      else exit_chunk<R, false, false>(S, c, lane, profLane, codeLane, bIn, col0, ts, qs, rs, cap);
+    }
+    if (capHere && lane == 0) {
+      ar[L.head + 4] = (int)(cap & kEMask);
+      ar[L.head + 5] = g;
+    }
+    // the bottom row (lane 63's last row) of steps t0 .. t0 + 63: columns t0 - 63 + lane
+    if (wantBot) {
+      const int j = c * 64 - 63 + lane;
+      if (j >= 0 && j <= n2) ebot[j] = (int)(S.Q & kEMask);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  }
+  // the segment's last frontier: the next segment's symbols point into it
+  if (g + 1 < L.G) {
+    int32_t* fr = ar + L.front + ((size_t)s * L.G + g) * F + lane;
+#pragma unroll
+    for (int k = 0; k < R; ++k) fr[k * 64] = (int)(S.Y[k] & kEMask);
+    fr[R * 64] = (int)(S.topPrev & kEMask);
+  }
+}
+
+// One workgroup per (pair, strip s in [1, start strip]): resolves the strip's frontiers segment
+// by segment (segment g's symbols refer to segment g - 1's last frontier), then the bottom row.
+template <int R>
+__global__ __launch_bounds__(256) void bg_exit_resolve_kernel(BgSplitArgs A) {
+  constexpr int F = (R + 1) * 64;
+  constexpr int kSym = BG_SPLIT_SYM(R);
+  __shared__ int fa[F], fb[F];
+  int p = 0;
+  const int item = blockIdx.x;
+  while (p + 1 < A.npairs && A.stripBase[p + 1] <= item) ++p;
+  const BgPair P = A.pairs[p];
+  const int n1 = P.n1, n2 = P.n2, NC = P.nc, NS = P.nstrips;
+  const BgSplitLayout L = bg_split_layout(n1, n2, NS, NC, R, A.segc);
+  const int s = 1 + (item - A.stripBase[p]);
+  int32_t* ar = A.split + P.split_off;
+  const int sStar = ar[L.head + 7];
+  if (s > sStar || s >= NS || ar[L.head + 6]) return;
+  const int tid = threadIdx.x;
+  const int32_t* fr = ar + L.front + (size_t)s * L.G * F;
+  int32_t* fs = ar + L.fres + (size_t)s * L.G * F;
+  int* prev = fa;
+  int* cur = fb;
+  for (int x = tid; x < F; x += blockDim.x) { prev[x] = fr[x]; fs[x] = fr[x]; }
+  __syncthreads();
+  for (int g = 1; g + 1 < L.G; ++g) {
+    for (int x = tid; x < F; x += blockDim.x) {
+      const int raw = fr[(size_t)g * F + x];
+      const int v = raw >= kSym ? prev[raw - kSym] : raw;
+      cur[x] = v;
+      fs[(size_t)g * F + x] = v;
+    }
+    __syncthreads();
+    int* t = prev; prev = cur; cur = t;
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (s < sStar) {
+    int32_t* eb = ar + L.ebot + (size_t)s * (n2 + 1);
+    for (int j = tid; j <= n2; j += blockDim.x) {
+      const int raw = eb[j];
+      if (raw >= kSym) {
+        const int seg = ((j + 63) >> 6) / A.segc;       // lane 63 is at column j at step j + 63
+        eb[j] = seg >= 1 ? fs[(size_t)(seg - 1) * F + (raw - kSym)] : -1;
+      }
+    }
+  }
+}
+
+// One wave per pair: the start cell's exit, then one lookup per strip up to the first strip
+// whose walk stops in it; writes every strip's start column (-1: not walked).
+template <int R>
+__global__ __launch_bounds__(64) void bg_exit_chain_kernel(BgSplitArgs A) {
+  constexpr int F = (R + 1) * 64;
+  constexpr int kSym = BG_SPLIT_SYM(R);
+  const BgPair P = A.pairs[blockIdx.x];
+  const int n1 = P.n1, n2 = P.n2, NC = P.nc, NS = P.nstrips;
+  if (NS == 0) return;
+  const BgSplitLayout L = bg_split_layout(n1, n2, NS, NC, R, A.segc);
+  int32_t* ar = A.split + P.split_off;
+  const int lane = threadIdx.x;
+  int sStar = ar[L.head + 7];
+  const bool over = ar[L.head + 6] != 0;
+  int lo = NS;                                           // strips lo .. sStar are walked
+  if (sStar >= 0 && !over) {
+    lo = sStar;
+    if (lane == 0) {
+      ar[L.startcol + sStar] = ar[L.head + 1];
+      if (sStar >= 1) {
+        int c = ar[L.head + 4];
+        const int cg = ar[L.head + 5];
+        if (c >= kSym) c = (cg >= 1 && cg < L.G) ? ar[L.fres + ((size_t)sStar * L.G + cg - 1) * F + (c - kSym)] : -1;
+        for (int s = sStar - 1; s >= 0; --s) {
+          if ((c <= 0 && A.mode != BGK_GLOBAL) || c < 0 || c > n2) break;
+          ar[L.startcol + s] = c;
+          lo = s;
+          if (s == 0) break;
+          c = ar[L.ebot + (size_t)s * (n2 + 1) + c];
+        }
+      }
+    }
+    lo = __shfl(lo, 0, 64);
+  } else if (lane == 0) {
+    ar[L.head + 7] = -1;
+    sStar = -1;
+  }
+  sStar = __shfl(sStar, 0, 64);
+  for (int s = lane; s < NS; s += 64)
+    if (s < lo || s > sStar) ar[L.startcol + s] = -1;
+}
+
+#define BG_SPLIT_INST(RR)                                                    \
+  template __global__ void bg_exit_kernel<RR>(BgSplitArgs);                 \
+  template __global__ void bg_exit_resolve_kernel<RR>(BgSplitArgs);         \
+  template __global__ void bg_exit_chain_kernel<RR>(BgSplitArgs);
+BG_SPLIT_INST(2)
+BG_SPLIT_INST(3)
+BG_SPLIT_INST(4)
+BG_SPLIT_INST(5)
+BG_SPLIT_INST(8)
+BG_SPLIT_INST(10)
+
+// which: 0 exit pass, 1 resolve, 2 chain
+extern "C" void* bg_split_kernel_ptr(int R, int which) {
+  switch (R) {
+#define BG_SPLIT_CASE(RR)                                                      \
+    case RR:                                                                   \
+      return which == 0 ? (void*)&bg_exit_kernel<RR>                           \
+           : which == 1 ? (void*)&bg_exit_resolve_kernel<RR>                   \
+                        : (void*)&bg_exit_chain_kernel<RR>;
+    BG_SPLIT_CASE(2)
+    BG_SPLIT_CASE(3)
+    BG_SPLIT_CASE(4)
+    BG_SPLIT_CASE(5)
+    BG_SPLIT_CASE(8)
+    BG_SPLIT_CASE(10)
+#undef BG_SPLIT_CASE
+    default: return nullptr;
+  }
+}
+// dynamic LDS of one exit-pass workgroup (4 waves)
+extern "C" int bg_exit_lds_bytes(int R) {
+  switch (R) {
+    case 2: return 4 * 4 * exit_wave_ints<2>();
+    case 3: return 4 * 4 * exit_wave_ints<3>();
+    case 4: return 4 * 4 * exit_wave_ints<4>();
+    case 5: return 4 * 4 * exit_wave_ints<5>();
+    case 8: return 4 * 4 * exit_wave_ints<8>();
+    case 10: return 4 * 4 * exit_wave_ints<10>();
+    default: return 0;
+  }
+}

@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--timing", action="store_true", help="finish-kernel cycle breakdown (stderr)")
     ap.add_argument("--rank", type=int, default=0, help="C4 / C5: the shard this GPU runs")
     ap.add_argument("--world", type=int, default=8, help="C4 / C5: GPUs the job is sharded over")
+    ap.add_argument("--single", type=int, default=0,
+                    help="also time N lone executes (execute + synchronize each): one alignment's wall")
     args = ap.parse_args()
     if args.timing:
         os.environ["BG_FINISH_TIMING"] = "1"
@@ -102,6 +104,26 @@ def main():
                 "dna": st["dna"], "bad_status": bad}
         if name in ("C4", "C5"):
             line["shard"] = "rank %d of %d (LPT by cells)" % (args.rank, args.world)
+        if args.single:
+            walls, dps, fins = [], [], []
+            for _ in range(args.single):
+                h.synchronize()
+                t0 = time.perf_counter()
+                h.execute()
+                h.synchronize()
+                walls.append((time.perf_counter() - t0) * 1e3)
+                s2 = h.stats()
+                dps.append(s2["dp_ms"])
+                fins.append(s2["finish_ms"])
+            walls.sort()
+            line["single"] = {"wall_ms_min": round(walls[0], 3), "wall_ms_median": round(walls[len(walls) // 2], 3),
+                              "dp_ms": round(sorted(dps)[len(dps) // 2], 3),
+                              "finish_ms": round(sorted(fins)[len(fins) // 2], 3),
+                              "gcups": round(st["cells"] / (walls[len(walls) // 2] * 1e-3) / 1e9, 2)}
+            try:
+                line["split_stats"] = h.split_stats()
+            except Exception:                         # noqa: BLE001 (older library)
+                pass
         if args.check:
             from oracle import refcpu
             k = min(args.check, len(pairs))
