@@ -115,7 +115,7 @@ def lib():
     L.bg_batch_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
                                  ctypes.c_size_t]
     L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
-    L.bg_split_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 4
+    L.bg_split_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 5
     L.bg_aligner_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.c_size_t)]
     L.bg_aligner_set_buffer_size.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t]
@@ -400,9 +400,9 @@ class Handle:
     def split_stats(self):
         """bg_split_stats: the last execute's split traceback (pairs split, strips stitched,
         moves the stitching walked itself, pairs whose exit pass overflowed)."""
-        v = [ctypes.c_uint64() for _ in range(4)]
+        v = [ctypes.c_uint64() for _ in range(5)]
         check(lib().bg_split_stats(self._p, *[ctypes.byref(x) for x in v]))
-        return dict(zip(("pairs_split", "strips_taken", "tail_moves", "pairs_overflow"),
+        return dict(zip(("pairs_split", "strips_taken", "tail_moves", "pairs_overflow", "items_beside_dp"),
                         (x.value for x in v)))
 
 

@@ -60,7 +60,7 @@ struct BgStripHdr {
 // area's start).  head: [0] end row, [1] end column, [2] score, [3] column case, [4] raw exit of
 // the start cell, [5] its segment, [6] overflow flag, [7] start strip (-1: nothing to split).
 struct BgSplitLayout {
-  uint64_t head, startcol, hdr, ebot, front, fres, ops, total_ints;
+  uint64_t head, startcol, hdr, ebot, front, fres, ckg, done, ops, total_ints;
   int32_t G, F, capS;
 };
 __host__ __device__ inline BgSplitLayout bg_split_layout(int n1, int n2, int nstrips, int nc, int R,
@@ -78,6 +78,10 @@ __host__ __device__ inline BgSplitLayout bg_split_layout(int n1, int n2, int nst
   L.ebot = o; o += (S * (uint64_t)(n2 + 1) + 15) / 16 * 16;
   L.front = o; o += S * (uint64_t)L.G * L.F;
   L.fres = o; o += S * (uint64_t)L.G * L.F;
+  // concurrent exit pass: the DP's segment-start checkpoints as {value, epoch} granules
+  // (8 bytes: two ints), and a done tag per exit-pass item
+  L.ckg = o; o += 2 * S * (uint64_t)L.G * L.F;
+  L.done = o; o += (S * (uint64_t)L.G + 15) / 16 * 16;
   L.ops = o * 4;
   o += (S * (uint64_t)L.capS + 63) / 64 * 16;
   L.total_ints = o;
@@ -95,6 +99,16 @@ struct BgSplitArgs {
   int32_t* split;          // the slot's split arena
   const int32_t* itemBase; // exit pass: first work item of each plan pair (npairs + 1)
   const int32_t* stripBase;// resolve: first workgroup (strips 1 .. nstrips - 1) of each plan pair
+  // concurrent exit pass (conc = 1: launched beside the DP, persistent workers taking items in
+  // `order` from *counter, inputs from the DP's epoch-tagged granules; conc = 0: the pass after
+  // the DP, skipping items whose done tag is this epoch)
+  int32_t conc;
+  uint32_t epoch;
+  const unsigned long long* gran;
+  const int32_t* order;
+  uint32_t* counter;
+  const uint32_t* resident;
+  int32_t dpWgs;
   int32_t npairs, nitems;
   int32_t open, ext, mode, R, segc;
   int32_t margin;          // headroom below a chunk's smallest input: clampv + max(0, max S - 2a) + 1
@@ -176,6 +190,12 @@ struct BgDpArgs {
                              // granules, indexed like bndM (zeroed when allocated)
   uint32_t epoch;          // this execute's granule tag (never 0, never reused by the handle)
   int32_t wide_pace;       // WIDE: s_sleep(1)s strip 0 adds per 32 steps (slack for the chain)
+  // split traceback with the exit pass running beside the DP (bg_split.hip): the slot's split
+  // arena (segment-start checkpoints as {value, epoch} granules, every strip's output row as
+  // granules too), the exit pass's segment length, and the resident-workgroup counter
+  int32_t* split;
+  int32_t segc;
+  uint32_t* resident;
 };
 
 struct BgFinishArgs {

@@ -34,6 +34,7 @@ extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt);
 extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode);
 extern "C" void* bg_split_kernel_ptr(int R, int which);
 extern "C" int bg_exit_lds_bytes(int R);
+extern "C" int bg_exit_conc_lds_bytes(int R);
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
 extern "C" int bg_dp_tag_wave_lds_bytes(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
@@ -132,8 +133,9 @@ struct PhaseTimer {
 // Per-execute arenas.  Two slots let the finish kernel of execute k (stream2) run while the
 // DP kernel of execute k+1 (stream) fills the other slot's trace.
 struct Slot {
-  DevBuf trace, bndM, bndX, aux, out1, out2, results, ops, gran, split;
+  DevBuf trace, bndM, bndX, aux, out1, out2, results, ops, gran, split, gprog;
   hipEvent_t dpDone = nullptr, finDone = nullptr;
+  hipEvent_t resetDone = nullptr;   // the DP's progress words zeroed (the concurrent exit pass waits)
   bool inflight = false;
 };
 
@@ -144,6 +146,10 @@ struct bg_aligner {
   hipStream_t stream2 = nullptr;   // end cell + traceback kernels
   hipStream_t stream3 = nullptr;   // WIDE batches: every other execute's traceback (see execute)
   hipStream_t stream4 = nullptr;   // WIDE batches at pipeline depth 4: every third one
+  // WIDE batches: every other execute's DP.  A WIDE DP holds one CU per group workgroup (C3: 79 of
+  // 256), so two executes' DPs run side by side on disjoint CUs (each waits for its own slot's
+  // previous traceback); created on first use, BG_ONE_DP_STREAM=1 keeps one
+  hipStream_t dps = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
   DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
   Slot slot[4];
@@ -193,7 +199,9 @@ struct bg_aligner {
   int splitItems = 0, splitResolve = 0;
   uint64_t splitInts = 0;
   std::vector<int2> splitMap;
-  std::vector<int32_t> splitBases;  // exit-pass item bases (np + 1), then resolve bases (np + 1)
+  std::vector<int32_t> splitBases;  // exit-pass item bases (np + 1), then resolve bases (np + 1),
+                                    // then the items in estimated readiness order (concurrent pass)
+  int splitConc = 0;                // the exit pass runs beside the DP (BG_SPLIT_CONC=0: after it)
   DevBuf splitMapBuf, splitBaseBuf;
   int tagRow = 0;                  // tagged kernel: the code row staged whole in LDS
   std::vector<int> groupOf;        // caller pair -> workgroups (WIDE)
@@ -231,7 +239,7 @@ struct bg_aligner {
                profScratch.cap;
     for (const Slot& S : slot)
       t += S.trace.cap + S.bndM.cap + S.bndX.cap + S.aux.cap + S.out1.cap + S.out2.cap + S.results.cap +
-           S.ops.cap + S.gran.cap + S.split.cap;
+           S.ops.cap + S.gran.cap + S.split.cap + S.gprog.cap;
     return t;
   }
 };
@@ -312,14 +320,18 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   if (h->stream3) (void)hipStreamSynchronize(h->stream3);
   if (h->stream4) (void)hipStreamSynchronize(h->stream4);
+  if (h->dps) (void)hipStreamSynchronize(h->dps);
   for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs,
                     &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg, &h->profScratch, &h->compactSizes})
     d->release();
   for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
   for (Slot& S : h->slot) {
-    for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops, &S.gran}) d->release();
+    for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops, &S.gran, &S.split,
+                      &S.gprog})
+      d->release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
     if (S.finDone) (void)hipEventDestroy(S.finDone);
+    if (S.resetDone) (void)hipEventDestroy(S.resetDone);
   }
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -329,6 +341,7 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->stream3) (void)hipStreamDestroy(h->stream3);
   if (h->stream4) (void)hipStreamDestroy(h->stream4);
+  if (h->dps) (void)hipStreamDestroy(h->dps);
   delete h;
 }
 
@@ -354,7 +367,8 @@ extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
   if (!h || depth < 1 || depth > 4) return BG_E_ARG;
   if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
       hipStreamSynchronize(h->stream2) != hipSuccess || hipStreamSynchronize(h->stream3) != hipSuccess ||
-      (h->stream4 && hipStreamSynchronize(h->stream4) != hipSuccess))
+      (h->stream4 && hipStreamSynchronize(h->stream4) != hipSuccess) ||
+      (h->dps && hipStreamSynchronize(h->dps) != hipSuccess))
     return BG_E_HIP;
   h->depth = depth;
   h->prepared = false;   // arenas are sized at prepare time
@@ -418,7 +432,8 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
   for (size_t p : comp) maxn1 = std::max(maxn1, n1[p]);
   if (maxn1 < 64 * 4 * 16) return false;                   // one workgroup's 16 waves suffice
   int W = 4;
-  if (const char* e = std::getenv("BG_WIDE_W")) W = std::max(1, std::min(16, std::atoi(e)));
+  // (the WIDE kernel is built for at most 4 waves per workgroup, bg_tag_kernel.hip)
+  if (const char* e = std::getenv("BG_WIDE_W")) W = std::max(1, std::min(4, std::atoi(e)));
   const int cand[] = {2, 3, 4, 5, 8, 10};
   double best = 1e300;
   int bestR = 0;
@@ -690,6 +705,7 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
   if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
+  if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
   tm.mark(kPhSync, "sync");
   for (Slot& S : h->slot) S.inflight = false;
   h->execCount = 0;
@@ -981,6 +997,24 @@ plan_again:
       }
       h->splitItems = h->splitBases[np];
       h->splitResolve = h->splitBases[2 * np + 1];
+      // the concurrent pass takes items in the order the DP makes them ready: strip s reaches
+      // chunk c at about (3 s + c) chunk times (a strip starts ~3 chunks after the one above)
+      {
+        const char* ec = std::getenv("BG_SPLIT_CONC");
+        h->splitConc = !(ec && ec[0] == '0');
+      }
+      std::vector<std::pair<int64_t, int32_t>> keyed;
+      keyed.reserve(h->splitItems);
+      for (size_t q = 0; q < np; ++q) {
+        const BgPair& P = h->plan[q];
+        const BgSplitLayout L = bg_split_layout(P.n1, P.n2, P.nstrips, P.nc, R, h->segc);
+        for (int s2 = 1; s2 < P.nstrips; ++s2)
+          for (int g = 0; g < L.G; ++g)
+            keyed.emplace_back(3LL * s2 + (int64_t)g * h->segc,
+                               h->splitBases[q] + (s2 - 1) * L.G + g);
+      }
+      std::stable_sort(keyed.begin(), keyed.end());
+      for (const auto& kv : keyed) h->splitBases.push_back(kv.second);
     }
   }
   h->traceBytes = tro;
@@ -1007,7 +1041,9 @@ plan_again:
         !S.bndX.ensure((h->affine || h->ack) ? bo * 4 + 256 : 256) || !S.aux.ensure(ao * 4 + 256) ||
         !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) || !S.ops.ensure(po + 16) ||
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)) ||
-        (h->split && !S.split.ensure(h->splitInts * 4 + 256)))
+        (h->split && S.split.cap < h->splitInts * 4 + 256 &&
+         (!S.split.ensure(h->splitInts * 4 + 256) || hipMemset(S.split.p, 0, S.split.cap) != hipSuccess)) ||
+        (h->wide && !S.gprog.ensure(4 * ((size_t)h->progWords + 2))))
       return BG_E_NOMEM;
     // WIDE checkpoint batches hand strip rows between workgroups as epoch-tagged granules: a
     // fresh arena is zeroed so that no stale tag (of another handle) can match an epoch
@@ -1161,14 +1197,21 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   const unsigned np = (unsigned)h->plan.size();
   const int z = h->execCount % h->depth;
   Slot& S = h->slot[z];
+  // the DP's stream: WIDE batches alternate two (see bg_aligner::dps)
+  hipStream_t ds = h->stream;
+  if (h->wide && h->depth >= 2 && (h->execCount & 1) && !std::getenv("BG_ONE_DP_STREAM") &&
+      !std::getenv("BG_DP_TIMING")) {
+    if (!h->dps && hipStreamCreateWithFlags(&h->dps, hipStreamNonBlocking) != hipSuccess) h->dps = nullptr;
+    if (h->dps) ds = h->dps;
+  }
   // the previous user of this slot must have finished reading its trace
-  if (S.inflight) BG_HIP(hipStreamWaitEvent(h->stream, S.finDone, 0));
+  if (S.inflight) BG_HIP(hipStreamWaitEvent(ds, S.finDone, 0));
   hipEvent_t e[4] = {h->ev[0], h->ev[1], h->ev[2], h->ev[3]};
   if (h->profiling && h->ringUsed + 4 <= (int)h->ring.size()) {
     for (int x = 0; x < 4; ++x) e[x] = h->ring[h->ringUsed + x];
     h->ringUsed += 4;
   }
-  BG_HIP(hipEventRecord(e[0], h->stream));
+  BG_HIP(hipEventRecord(e[0], ds));
   if (np) {
     void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : dp_fn(h, h->R);
     if (!fn) return BG_E_ARG;
@@ -1184,13 +1227,17 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.codes_in_lds = h->codesInLds;
     A.aux_lds_off = h->auxLdsOff;
     A.wgmap = h->wgmapBuf.as<int2>();
-    A.gprog = h->gprogBuf.as<uint32_t>();
+    A.gprog = h->wide ? S.gprog.as<uint32_t>() : h->gprogBuf.as<uint32_t>();
     A.dbg = nullptr;
     if (std::getenv("BG_DP_TIMING") && h->tag && h->dpDbg.ensure(64 * 4096)) {
       A.dbg = h->dpDbg.as<unsigned long long>();
-      BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, h->stream));
+      BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, ds));
     }
-    if (h->wide) BG_HIP(hipMemsetAsync(h->gprogBuf.p, 0, 4 * (size_t)h->progWords, h->stream));
+    if (h->wide) BG_HIP(hipMemsetAsync(S.gprog.p, 0, 4 * ((size_t)h->progWords + 2), ds));
+    if (h->split && h->splitConc) {
+      if (!S.resetDone) BG_HIP(hipEventCreateWithFlags(&S.resetDone, hipEventDisableTiming));
+      BG_HIP(hipEventRecord(S.resetDone, ds));
+    }
     A.prof_scratch = h->pglob ? h->profScratch.as<int32_t>() : nullptr;
     if (++h->epoch == 0) h->epoch = 1;
     A.epoch = h->epoch;
@@ -1199,6 +1246,9 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       A.wide_pace = ev ? std::atoi(ev) : 0;
     }
     A.gran = S.gran.as<unsigned long long>();
+    A.split = (h->split && h->splitConc) ? S.split.as<int32_t>() : nullptr;
+    A.segc = h->segc;
+    A.resident = h->wide ? S.gprog.as<uint32_t>() + h->progWords : nullptr;
     A.trace = S.trace.as<uint32_t>();
     A.bndM = S.bndM.as<int32_t>();
     A.bndX = S.bndX.as<int32_t>();
@@ -1213,10 +1263,10 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     void* args[] = {&A};
     if (h->lds > 65536)
       BG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds));
-    BG_HIP(hipLaunchKernel(fn, dim3(h->gridWgs), dim3(64 * h->W), args, h->lds, h->stream));
+    BG_HIP(hipLaunchKernel(fn, dim3(h->gridWgs), dim3(64 * h->W), args, h->lds, ds));
   }
-  BG_HIP(hipEventRecord(e[1], h->stream));
-  BG_HIP(hipEventRecord(S.dpDone, h->stream));
+  BG_HIP(hipEventRecord(e[1], ds));
+  BG_HIP(hipEventRecord(S.dpDone, ds));
   // The traceback stream.  A WIDE batch (a few long pairs: C3) is traceback-bound and its walks
   // occupy a handful of CUs, so consecutive executes' tracebacks alternate between two streams
   // and run side by side (each still waits for its own DP; the slot it reads is not reused before
@@ -1237,6 +1287,50 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   const hipStream_t fss[3] = {h->stream2, h->stream3, h->stream4};
   hipStream_t fs = fss[h->execCount % nfs];
+  // split traceback: its arguments, and the exit pass beside the DP (it waits for the DP's
+  // progress words to be zeroed, then takes items as the DP makes them ready)
+  BgSplitArgs X;
+  std::memset(&X, 0, sizeof(X));
+  if (np && h->split) {
+    X.pairs = h->pairs.as<BgPair>();
+    X.codes1 = h->codes1.as<uint8_t>();
+    X.codes2 = h->codes2.as<uint8_t>();
+    X.ckpt = S.trace.as<int32_t>();
+    X.bndM = S.bndM.as<int32_t>();
+    X.profile = h->prof.as<int32_t>();
+    X.split = S.split.as<int32_t>();
+    X.itemBase = h->splitBaseBuf.as<int32_t>();
+    X.stripBase = h->splitBaseBuf.as<int32_t>() + (np + 1);
+    X.order = h->splitBaseBuf.as<int32_t>() + 2 * (np + 1);
+    X.npairs = (int32_t)np;
+    X.nitems = h->splitItems;
+    X.open = h->a;
+    X.ext = h->b;
+    X.mode = h->mode;
+    X.R = h->R;
+    X.segc = h->segc;
+    X.margin = h->splitMargin;
+    X.clampv = h->splitClamp;
+    X.grow = h->splitGrow;
+    X.epoch = h->epoch;
+    X.gran = S.gran.as<unsigned long long>();
+    X.resident = S.gprog.as<uint32_t>() + h->progWords;
+    X.counter = S.gprog.as<uint32_t>() + h->progWords + 1;
+    X.dpWgs = h->gridWgs;
+    if (h->splitConc && h->splitItems > 0) {
+      X.conc = 1;
+      void* cargs[] = {&X};
+      void* cfn = bg_split_kernel_ptr(h->R, 3);
+      // more than half a CU's LDS: never beside a WIDE DP workgroup (which claims over half too)
+      const size_t clds = std::max<size_t>((size_t)bg_exit_conc_lds_bytes(h->R), 80 * 1024 + 64);
+      BG_HIP(hipFuncSetAttribute(cfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds));
+      BG_HIP(hipStreamWaitEvent(fs, S.resetDone, 0));
+      // one workgroup per CU the DP leaves free: even dispatched first, they leave the DP its CUs
+      const int cg = std::max(1, h->cus - h->gridWgs);
+      BG_HIP(hipLaunchKernel(cfn, dim3(cg), dim3(h->R >= 8 ? 512 : 1024), cargs, clds, fs));
+      X.conc = 0;
+    }
+  }
   BG_HIP(hipStreamWaitEvent(fs, S.dpDone, 0));
   BG_HIP(hipEventRecord(e[2], fs));
   if (np) {
@@ -1303,28 +1397,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       if (!h->split) {
         BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
       } else {
-        // split traceback: end cell -> exit pass -> per-strip resolve -> chain ->
-        // the strips' walks in parallel -> stitch + strings
-        BgSplitArgs X;
-        X.pairs = F.pairs;
-        X.codes1 = F.codes1;
-        X.codes2 = F.codes2;
-        X.ckpt = reinterpret_cast<const int32_t*>(F.trace);
-        X.bndM = F.bndM;
-        X.profile = F.profile;
-        X.split = F.split;
-        X.itemBase = h->splitBaseBuf.as<int32_t>();
-        X.stripBase = h->splitBaseBuf.as<int32_t>() + (np + 1);
-        X.npairs = (int32_t)np;
-        X.nitems = h->splitItems;
-        X.open = h->a;
-        X.ext = h->b;
-        X.mode = h->mode;
-        X.R = h->R;
-        X.segc = h->segc;
-        X.margin = h->splitMargin;
-        X.clampv = h->splitClamp;
-        X.grow = h->splitGrow;
+        // split traceback: end cell -> exit pass (the items the pass beside the DP
+        // did not do) -> per-strip resolve -> chain -> the strips' walks in parallel -> stitch
         void* xargs[] = {&X};
         F.phase = BG_PH_HEAD;
         BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
@@ -1366,6 +1440,7 @@ extern "C" int bg_synchronize(bg_aligner* h) {
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
   if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
+  if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
   if (h->executed) {
     (void)hipEventElapsedTime(&h->dp_ms, h->last[0], h->last[1]);
     (void)hipEventElapsedTime(&h->fin_ms, h->last[2], h->last[3]);
@@ -1522,9 +1597,9 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
 }
 
 extern "C" int bg_split_stats(bg_aligner* h, uint64_t* pairs_split, uint64_t* strips_taken,
-                              uint64_t* tail_moves, uint64_t* pairs_overflow) {
-  if (!h || !pairs_split || !strips_taken || !tail_moves || !pairs_overflow) return BG_E_ARG;
-  *pairs_split = *strips_taken = *tail_moves = *pairs_overflow = 0;
+                              uint64_t* tail_moves, uint64_t* pairs_overflow, uint64_t* items_beside_dp) {
+  if (!h || !pairs_split || !strips_taken || !tail_moves || !pairs_overflow || !items_beside_dp) return BG_E_ARG;
+  *pairs_split = *strips_taken = *tail_moves = *pairs_overflow = *items_beside_dp = 0;
   if (!h->split || !h->executed) return BG_OK;
   const int rc = bg_synchronize(h);
   if (rc) return rc;
@@ -1532,7 +1607,13 @@ extern "C" int bg_split_stats(bg_aligner* h, uint64_t* pairs_split, uint64_t* st
   for (const BgPair& P : h->plan) {
     int32_t head[16];
     BG_HIP(hipMemcpy(head, S.split.as<int32_t>() + P.split_off, sizeof(head), hipMemcpyDeviceToHost));
-    if (head[6]) ++*pairs_overflow;
+    if (head[6] || (uint32_t)head[11] == h->epoch) ++*pairs_overflow;
+    const BgSplitLayout L = bg_split_layout(P.n1, P.n2, P.nstrips, P.nc, h->R, h->segc);
+    if (P.nstrips > 1) {
+      std::vector<uint32_t> dn((size_t)(P.nstrips - 1) * L.G);
+      BG_HIP(hipMemcpy(dn.data(), S.split.as<int32_t>() + P.split_off + L.done, dn.size() * 4, hipMemcpyDeviceToHost));
+      for (uint32_t v : dn) *items_beside_dp += v == h->epoch;
+    }
     if (head[7] >= 0) ++*pairs_split;
     if (head[7] >= 0 && head[8] > 0) *strips_taken += (uint64_t)head[8];
     if (head[7] >= 0 && head[10] > 0) *tail_moves += (uint64_t)head[10];
@@ -1585,6 +1666,7 @@ extern "C" int bg_profile_end(bg_aligner* h, float* avg_dp, float* avg_fin, int*
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
   if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
+  if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
   double dp = 0, fin = 0;
   const int cnt = h->ringUsed / 4;
   for (int i = 0; i < cnt; ++i) {
@@ -1612,6 +1694,7 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   BG_HIP(hipStreamSynchronize(h->stream2));
   BG_HIP(hipStreamSynchronize(h->stream3));
   if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
+  if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
   const Slot& S = h->slot[h->lastSlot];
   const uint64_t n = h->npairs;
   BG_HIP(hipMemcpyAsync(dst, &n, 8, hipMemcpyHostToDevice, h->stream));
@@ -1659,6 +1742,7 @@ extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) 
     BG_HIP(hipStreamSynchronize(h->stream2));
     BG_HIP(hipStreamSynchronize(h->stream3));
     if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
+    if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
     BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), h->stream));
     const unsigned g = (unsigned)(((uint64_t)E.nplan + 255) / 256);
     if (g) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(g), dim3(256), args, 0, h->stream));

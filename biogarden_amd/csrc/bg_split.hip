@@ -148,22 +148,23 @@ __device__ __forceinline__ void exit_chunk(ExitStrip<R>& S, int c, int lane, con
 
 }  // namespace
 
-// One wave per (pair, strip s >= 1, segment g).  Outputs (split area of the pair):
-//   ebot[s][j]        raw exit of the strip's bottom row at column j (strips s < start strip)
+// One exit-pass item: a wave runs (pair, strip s >= 1, segment g).  Outputs (split area):
+//   ebot[s][j]        raw exit of the strip's bottom row at column j
 //   front[s][g][x]    raw exits of the segment's last frontier, x = k * 64 + lane (k < R: the
 //                     lane's rows; k = R: its top-left input), for segment g + 1's symbols
-//   head[4], head[5]  raw exit of the walk's start cell and its segment (start strip only)
-//   head[6]           set when a chunk's values could leave the packed field
-template <int R>
-__global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
-  extern __shared__ __attribute__((aligned(16))) int esm[];
+//   head[4], head[5]  raw exit of the walk's start cell and its segment (start strip, after the DP)
+//   head[6]           set when a chunk's values could leave the packed field (head[11] = epoch:
+//                     the same, from the concurrent pass)
+// CONC: the pass beside the DP.  Its inputs are the DP's {value, epoch} granules (the segment's
+// start checkpoint, the output row of the strip above), read agent-coherent and waited for until
+// every tag is this execute's epoch; the start strip and cell are not known yet, so every strip's
+// bottom row is kept and nothing is captured.  The item's done tag then lets the pass after the
+// DP skip it.
+template <int R, bool CONC>
+__device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
   constexpr int ROWS = 64 * R;
   constexpr int F = (R + 1) * 64;
   constexpr unsigned kSym = BG_SPLIT_SYM(R);
-  const int lane = threadIdx.x & 63;
-  const int w = uni(threadIdx.x >> 6);
-  const int item = uni((int)blockIdx.x * 4 + w);
-  if (item >= A.nitems) return;
   int p = 0;
   while (p + 1 < A.npairs && A.itemBase[p + 1] <= item) ++p;
   p = uni(p);
@@ -173,13 +174,20 @@ __global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
   const int rel = item - A.itemBase[p];
   const int s = 1 + rel / L.G, g = rel % L.G;
   int32_t* ar = A.split + P.split_off;
-  const int sStar = uni(ar[L.head + 7]);
+  const int sStar = CONC ? NS - 1 : uni(ar[L.head + 7]);
   if (s > sStar || s >= NS) return;
   const int c0 = g * A.segc;
   const int c1 = min(NC, c0 + A.segc);
   const int a = A.open, b = A.ext, mode = A.mode;
+  // the start cell, when it lies in this strip (lane rs, row qs, step ts): after the DP only
+  const int ei = CONC ? 0 : ar[L.head + 0], ej = CONC ? 0 : ar[L.head + 1];
+  const bool capStrip = !CONC && (s == sStar) && ei >= 1 && ej >= 1;
+  const int vs = ei - 1 - s * ROWS;
+  const int rs = capStrip ? vs / R : 0, qs = capStrip ? vs % R : 0, ts = capStrip ? ej + rs : -1;
+  const bool capItem = capStrip && ts >= c0 * 64 && ts < c1 * 64;
+  uint32_t* done = reinterpret_cast<uint32_t*>(ar + L.done);
+  if (!CONC && !capItem && done[(size_t)(s - 1) * L.G + g] == A.epoch) return;   // done beside the DP
 
-  int* wl = esm + w * exit_wave_ints<R>();
   int* prof = wl;                                       // [code][k][lane]
   unsigned* bIn = reinterpret_cast<unsigned*>(wl + 4 * R * 64);
   uint16_t* stage = reinterpret_cast<uint16_t*>(wl + 4 * R * 64 + 64);
@@ -200,14 +208,24 @@ __global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
   }
   const int* profLane = prof + lane;
   const uint16_t* codeLane = stage + 63 - lane;
-  // the start cell, when it lies in this strip (lane rs, row qs, step ts)
-  const int ei = ar[L.head + 0], ej = ar[L.head + 1];
-  const bool capStrip = (s == sStar) && ei >= 1 && ej >= 1;
-  const int vs = ei - 1 - s * ROWS;
-  const int rs = capStrip ? vs / R : 0, qs = capStrip ? vs % R : 0, ts = capStrip ? ej + rs : -1;
-  const int32_t* topRow = A.bndM + P.bnd_off + (size_t)(s - 1) * NC * 64;   // M'(s*ROWS, j)
+  const size_t topOff = P.bnd_off + (size_t)(s - 1) * NC * 64;        // M'(s*ROWS, j)
+  const int32_t* topRow = A.bndM + topOff;
+  const unsigned long long* topGran = A.gran + topOff;
   const int tclamp = n2 < NC * 64 - 1 ? n2 : NC * 64 - 1;
-  auto top_abs = [&](int c) { const int j = c * 64 + lane; return topRow[j <= tclamp ? j : tclamp]; };
+  // the top block of chunk c (columns c*64 + lane, clamped to n2)
+  auto top_abs = [&](int c) {
+    const int j = min(c * 64 + lane, tclamp);
+    if constexpr (!CONC) {
+      return topRow[j];
+    } else {
+      unsigned long long v = __hip_atomic_load(topGran + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      while (!__all((uint32_t)(v >> 32) == A.epoch)) {
+        __builtin_amdgcn_s_sleep(8);
+        v = __hip_atomic_load(topGran + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return (int)(uint32_t)v;
+    }
+  };
 
   // initial state: the segment's first checkpoint (absolute M'), or the strip start
   int Yabs[R], tpAbs;
@@ -222,16 +240,39 @@ __global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
     tpAbs = Yabs[0];                                     // never read by a valid cell
     tpE = 0;
   } else {
-    const int32_t* ck = A.ckpt + P.trace_off / 4 + ((size_t)(s * NC + c0) * (R + 1)) * 64 + lane;
+    if constexpr (!CONC) {
+      const int32_t* ck = A.ckpt + P.trace_off / 4 + ((size_t)(s * NC + c0) * (R + 1)) * 64 + lane;
 #pragma unroll
-    for (int k = 0; k < R; ++k) { Yabs[k] = ck[k * 64]; Ye[k] = kSym + (unsigned)(k * 64 + lane); }
-    tpAbs = ck[R * 64];
+      for (int k = 0; k < R; ++k) Yabs[k] = ck[k * 64];
+      tpAbs = ck[R * 64];
+    } else {
+      const unsigned long long* cg =
+          reinterpret_cast<const unsigned long long*>(ar + L.ckg) + (((size_t)s * L.G + g) * (R + 1)) * 64 + lane;
+      unsigned long long v[R + 1];
+      bool ok;
+      do {
+#pragma unroll
+        for (int k = 0; k <= R; ++k) v[k] = __hip_atomic_load(cg + k * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool mine = true;
+#pragma unroll
+        for (int k = 0; k <= R; ++k) mine = mine && (uint32_t)(v[k] >> 32) == A.epoch;
+        ok = __all(mine);
+        if (!ok) __builtin_amdgcn_s_sleep(8);
+      } while (!ok);
+#pragma unroll
+      for (int k = 0; k < R; ++k) Yabs[k] = (int)(uint32_t)v[k];
+      tpAbs = (int)(uint32_t)v[R];
+    }
+#pragma unroll
+    for (int k = 0; k < R; ++k) Ye[k] = kSym + (unsigned)(k * 64 + lane);
     tpE = lane == 0 ? (unsigned)(c0 * 64 - 1) : kSym + (unsigned)(R * 64 + lane);
   }
+  int* overflow = ar + L.head + (CONC ? 11 : 6);
+  const int ovVal = CONC ? (int)A.epoch : 1;
   int mt = top_abs(c0);
   ExitStrip<R> S;
   int base = 0;
-  // field value of an absolute M' (0 for a clamped column-0 value)
+  // field value of an absolute M' (clampv for a clamped column-0 value)
   auto fld = [&](int x) { return (unsigned)max(x - base, A.clampv) << kVShift; };
   {
     // the lanes' frontier cells sit at column c0 * 64 - 1 - lane, the top block at c0 * 64 + lane
@@ -245,7 +286,7 @@ __global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
     lo = uni(wave_min(lo));
     hi = uni(wave_max(hi));
     base = lo - A.margin;
-    if ((long)hi - base + A.grow > kVMax) { if (lane == 0) ar[L.head + 6] = 1; return; }
+    if ((long)hi - base + A.grow > kVMax) { if (lane == 0) *overflow = ovVal; return; }
 #pragma unroll
     for (int k = 0; k < R; ++k) S.Y[k] = fld(Yabs[k]) | kT3 | Ye[k];
     S.topPrev = fld(tpAbs) | kT2 | tpE;
@@ -270,7 +311,7 @@ __global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
       lo = uni(wave_min(lo));
       hi = uni(wave_max(hi));
       const int d = lo - A.margin;                       // new base - old base
-      if ((long)hi - d + A.grow > kVMax) { if (lane == 0) ar[L.head + 6] = 1; return; }
+      if ((long)hi - d + A.grow > kVMax) { if (lane == 0) *overflow = ovVal; return; }
       auto reb = [&](unsigned v) {
         return ((unsigned)max((int)(v >> kVShift) - d, A.clampv) << kVShift) | (v & ((1u << kVShift) - 1));
       };
@@ -322,6 +363,45 @@ __global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
     for (int k = 0; k < R; ++k) fr[k * 64] = (int)(S.Y[k] & kEMask);
     fr[R * 64] = (int)(S.topPrev & kEMask);
   }
+  if constexpr (CONC) {
+    __threadfence();
+    if (lane == 0) done[(size_t)(s - 1) * L.G + g] = A.epoch;
+  }
+}
+
+// The pass after the DP: one wave per item (4 per workgroup).
+template <int R>
+__global__ __launch_bounds__(256) void bg_exit_kernel(BgSplitArgs A) {
+  extern __shared__ __attribute__((aligned(16))) int esm[];
+  const int lane = threadIdx.x & 63;
+  const int w = uni(threadIdx.x >> 6);
+  const int item = uni((int)blockIdx.x * 4 + w);
+  if (item >= A.nitems) return;
+  exit_item<R, false>(A, item, lane, esm + w * exit_wave_ints<R>());
+}
+
+// The pass beside the DP: persistent workgroups (more than half a CU's LDS each, so none shares a
+// CU with a WIDE DP workgroup), every wave taking items in readiness order.  A worker waits for the
+// DP's data only once every DP workgroup is resident (else it leaves the items to the pass after
+// the DP): it can then never hold a CU the DP still needs.
+template <int R>
+__global__ __launch_bounds__(R >= 8 ? 512 : 1024) void bg_exit_conc_kernel(BgSplitArgs A) {
+  extern __shared__ __attribute__((aligned(16))) int esm[];
+  const int lane = threadIdx.x & 63;
+  const int w = uni(threadIdx.x >> 6);
+  int polls = 0;
+  while (__hip_atomic_load(A.resident, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)A.dpWgs) {
+    if (++polls > 4000) return;                          // ~0.25 ms: the DP has not started
+    __builtin_amdgcn_s_sleep(16);
+  }
+  int* wl = esm + w * exit_wave_ints<R>();
+  for (;;) {
+    int idx = 0;
+    if (lane == 0) idx = (int)__hip_atomic_fetch_add(A.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    idx = uni(__shfl(idx, 0, 64));
+    if (idx >= A.nitems) return;
+    exit_item<R, true>(A, A.order[idx], lane, wl);
+  }
 }
 
 // One workgroup per (pair, strip s in [1, start strip]): resolves the strip's frontiers segment
@@ -340,7 +420,7 @@ __global__ __launch_bounds__(256) void bg_exit_resolve_kernel(BgSplitArgs A) {
   const int s = 1 + (item - A.stripBase[p]);
   int32_t* ar = A.split + P.split_off;
   const int sStar = ar[L.head + 7];
-  if (s > sStar || s >= NS || ar[L.head + 6]) return;
+  if (s > sStar || s >= NS || ar[L.head + 6] || (uint32_t)ar[L.head + 11] == A.epoch) return;
   const int tid = threadIdx.x;
   const int32_t* fr = ar + L.front + (size_t)s * L.G * F;
   int32_t* fs = ar + L.fres + (size_t)s * L.G * F;
@@ -385,7 +465,7 @@ __global__ __launch_bounds__(64) void bg_exit_chain_kernel(BgSplitArgs A) {
   int32_t* ar = A.split + P.split_off;
   const int lane = threadIdx.x;
   int sStar = ar[L.head + 7];
-  const bool over = ar[L.head + 6] != 0;
+  const bool over = ar[L.head + 6] != 0 || (uint32_t)ar[L.head + 11] == A.epoch;
   int lo = NS;                                           // strips lo .. sStar are walked
   if (sStar >= 0 && !over) {
     lo = sStar;
@@ -416,6 +496,7 @@ __global__ __launch_bounds__(64) void bg_exit_chain_kernel(BgSplitArgs A) {
 
 #define BG_SPLIT_INST(RR)                                                    \
   template __global__ void bg_exit_kernel<RR>(BgSplitArgs);                 \
+  template __global__ void bg_exit_conc_kernel<RR>(BgSplitArgs);            \
   template __global__ void bg_exit_resolve_kernel<RR>(BgSplitArgs);         \
   template __global__ void bg_exit_chain_kernel<RR>(BgSplitArgs);
 BG_SPLIT_INST(2)
@@ -425,14 +506,15 @@ BG_SPLIT_INST(5)
 BG_SPLIT_INST(8)
 BG_SPLIT_INST(10)
 
-// which: 0 exit pass, 1 resolve, 2 chain
+// which: 0 exit pass, 1 resolve, 2 chain, 3 exit pass beside the DP
 extern "C" void* bg_split_kernel_ptr(int R, int which) {
   switch (R) {
 #define BG_SPLIT_CASE(RR)                                                      \
     case RR:                                                                   \
       return which == 0 ? (void*)&bg_exit_kernel<RR>                           \
            : which == 1 ? (void*)&bg_exit_resolve_kernel<RR>                   \
-                        : (void*)&bg_exit_chain_kernel<RR>;
+           : which == 2 ? (void*)&bg_exit_chain_kernel<RR>                     \
+                        : (void*)&bg_exit_conc_kernel<RR>;
     BG_SPLIT_CASE(2)
     BG_SPLIT_CASE(3)
     BG_SPLIT_CASE(4)
@@ -441,6 +523,19 @@ extern "C" void* bg_split_kernel_ptr(int R, int which) {
     BG_SPLIT_CASE(10)
 #undef BG_SPLIT_CASE
     default: return nullptr;
+  }
+}
+// dynamic LDS of one workgroup of the concurrent exit pass (16 waves, 8 from R = 8)
+extern "C" int bg_exit_conc_lds_bytes(int R) {
+  const int w = R >= 8 ? 8 : 16;
+  switch (R) {
+    case 2: return w * 4 * exit_wave_ints<2>();
+    case 3: return w * 4 * exit_wave_ints<3>();
+    case 4: return w * 4 * exit_wave_ints<4>();
+    case 5: return w * 4 * exit_wave_ints<5>();
+    case 8: return w * 4 * exit_wave_ints<8>();
+    case 10: return w * 4 * exit_wave_ints<10>();
+    default: return 0;
   }
 }
 // dynamic LDS of one exit-pass workgroup (4 waves)

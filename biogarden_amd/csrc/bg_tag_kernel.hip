@@ -114,8 +114,10 @@ __host__ __device__ constexpr int tag_wave_ints() {
 // CKPT: the score-only forward pass of the checkpoint traceback (score_chunk, untagged M'
 // values); at every chunk start each lane stores its R values and topPrev to the checkpoint
 // arena: ckpt[((s * NC + c) * (R + 1) + k) * 64 + lane] (k = R: topPrev).
+// WIDE: one workgroup of 4 waves per CU (one per SIMD), so a wave may hold up to 512 VGPRs: the
+// six conveyor-loop instantiations then run without spills (at 1024 threads they spilled 48 B/lane)
 template <int R, bool WIDE, bool CKPT>
-__global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
+__global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int RW = ProfW<R>::v;
   const int lane = threadIdx.x & 63;
@@ -163,7 +165,19 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
 
   const BgPair P = A.pairs[pairIdx];
   const int n1 = P.n1, n2 = P.n2, nst = P.nstrips, NC = P.nc;
+  // concurrent exit pass (bg_split.hip): it waits for this DP's data only once every workgroup of
+  // the DP is resident, so its workers can never hold the CUs this DP still needs
+  const bool ckgOn = WIDE && CKPT && A.split != nullptr;
+  if (ckgOn && threadIdx.x == 0) __hip_atomic_fetch_add(A.resident, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (nst == 0) return;
+  // its inputs: every segc-th checkpoint of each strip as {value, epoch} granules
+  unsigned long long* ckgPair = nullptr;
+  int ckgG = 1;
+  if (ckgOn) {
+    const BgSplitLayout SLy = bg_split_layout(n1, n2, nst, NC, R, A.segc);
+    ckgPair = reinterpret_cast<unsigned long long*>(A.split + P.split_off + SLy.ckg);
+    ckgG = SLy.G;
+  }
   const int GW = (WIDE ? P.wg_count : 1) * W;                  // waves working on this pair
   const int gw = gi * W + w;
   uint32_t* gProg = WIDE ? A.gprog + P.prog_off : nullptr;
@@ -315,6 +329,9 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       const rsrc_t rGo = uniform_rsrc(gOut, NC * BG_CHUNK * 8);
       const int vL4 = lane * 4, vH4 = l32 * 4, vH8 = l32 * 8;
       const rsrc_t rGi = uniform_rsrc(s > 0 ? gIn : gOut, NC * BG_CHUNK * 8);
+      // concurrent exit pass: segment-start checkpoints of this strip ({value, epoch}, [g][k][lane])
+      const rsrc_t rCkg = uniform_rsrc(ckgOn ? ckgPair + (size_t)s * ckgG * (R + 1) * BG_WAVE : gOut,
+                                       ckgOn ? ckgG * (R + 1) * BG_WAVE * 8 : 8);
       // two halves in flight: even halves in gvA, odd halves in gvB (the two boundary call sites
       // of a chunk), so a load has two halves' time to land and is never copied while pending
       u32x2 gvA = {0u, 0u}, gvB = {0u, 0u};
@@ -323,8 +340,9 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
       int kv = 0;
       u32x2 kg = {0u, 0u};
       int ckv[R + 1];
+      u32x2 ckgv[R + 1];                                         // concurrent exit pass granules
 #pragma unroll
-      for (int k = 0; k <= R; ++k) ckv[k] = 0;
+      for (int k = 0; k <= R; ++k) { ckv[k] = 0; ckgv[k] = u32x2{0u, 0u}; }
       int Q = 0;
       unsigned long long tData = 0, tFlow = 0;                   // BG_DP_TIMING: spin cycles
       // LDS words read a boundary ahead (their latency hides behind the half's compute; the
@@ -354,6 +372,13 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
         } else {
           kg = u32x2{(unsigned)v, ep};
           if (!lo) __builtin_amdgcn_raw_buffer_store_b64(kg, rGo, vH8, og * 256, kSC1);
+        }
+        if constexpr (MOUT) {
+          // the concurrent exit pass reads every strip's row from the granules
+          if (ckgOn) {
+            kg = u32x2{(unsigned)v, ep};
+            if (!lo) __builtin_amdgcn_raw_buffer_store_b64(kg, rGo, vH8, og * 256, kSC1);
+          }
         }
         kv = v;
         if (!lo) __builtin_amdgcn_raw_buffer_store_b32(kv, rBnd, vH4, og * 128, 0);
@@ -424,11 +449,20 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
           asm volatile("" : "+v"(ckv[k]));                    // a register of its own
           __builtin_amdgcn_raw_buffer_store_b32(ckv[k], rCk, vL4, (c * (R + 1) + k) * BG_WAVE * 4, 0);
         }
+        if (ckgOn && c % A.segc == 0) {
+          const int gseg = c / A.segc;
+#pragma unroll
+          for (int k = 0; k <= R; ++k) {
+            ckgv[k] = u32x2{(unsigned)ckv[k], ep};
+            asm volatile("" : "+v"(ckgv[k]));               // registers of their own (see ckv)
+            __builtin_amdgcn_raw_buffer_store_b64(ckgv[k], rCkg, vL4 * 2, ((gseg * (R + 1) + k) * BG_WAVE) * 8, kSC1);
+          }
+        }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         boundary(2 * c, gvA);
         auto mid = [&]() {
 #pragma unroll
-          for (int k = 0; k <= R; ++k) asm volatile("" ::"v"(ckv[k]));
+          for (int k = 0; k <= R; ++k) asm volatile("" ::"v"(ckv[k]), "v"(ckgv[k].x), "v"(ckgv[k].y));
           boundary(2 * c + 1, gvB);
         };
         const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
@@ -567,6 +601,14 @@ __global__ __launch_bounds__(1024) void bg_dp_tag_kernel(BgDpArgs A) {
 #pragma unroll
         for (int k = 0; k < R; ++k) ck[k * BG_WAVE] = S.Y[k];
         ck[R * BG_WAVE] = S.topPrev;
+        if (ckgOn && c % A.segc == 0) {
+          unsigned long long* cg = ckgPair + (((size_t)s * ckgG + c / A.segc) * (R + 1)) * BG_WAVE + lane;
+#pragma unroll
+          for (int k = 0; k <= R; ++k)
+            __hip_atomic_store(cg + k * BG_WAVE,
+                               ((unsigned long long)A.epoch << 32) | (uint32_t)(k < R ? S.Y[k] : S.topPrev),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         if (edge) score_chunk<R, TV_EDGE, WIDE>(S, C, c);
         else if (lastStrip && selRow) score_chunk<R, TV_SEL, WIDE>(S, C, c);
         else if (R <= 4 && s == 0) {

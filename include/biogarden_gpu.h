@@ -165,11 +165,11 @@ int bg_get_stats(bg_aligner* h, bg_stats* out);
 
 /* Split traceback of the last execute (few long pairs, linear gaps): pairs whose
  * walk was cut at strip boundaries, strips whose walks the stitching took, traceback moves the
- * stitching had to walk itself (0 when every strip walk was used), and pairs whose exit pass left
- * its packed range (walked whole).  All 0 when the batch is not split.  Waits for the handle's
- * work.  The results never depend on it: this is a diagnostic. */
+ * stitching had to walk itself (0 when every strip walk was used), pairs whose exit pass left its
+ * packed range (walked whole), and exit-pass items done beside the DP.  All 0 when the batch is
+ * not split.  Waits for the handle's work.  The results never depend on it: a diagnostic. */
 int bg_split_stats(bg_aligner* h, uint64_t* pairs_split, uint64_t* strips_taken,
-                   uint64_t* tail_moves, uint64_t* pairs_overflow);
+                   uint64_t* tail_moves, uint64_t* pairs_overflow, uint64_t* items_beside_dp);
 
 /* The reference aligner's scratch dims this handle models (SequenceAligner::buffer_size,
  * aligner.rs:30): 1024 x 1024 after bg_aligner_new (:44-55); every alignment call of a prepared

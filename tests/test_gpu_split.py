@@ -118,3 +118,41 @@ def test_split_global_column0_paths(oracle):
     got, st, sp = _run(pairs, "global", -1, -2)
     _check(oracle, "global", pairs, got, -1, -2)
     assert st["split"] == 1 and sp["tail_moves"] == 0, sp
+
+
+def test_split_exit_pass_beside_dp(oracle, monkeypatch):
+    """The exit pass beside the DP (persistent workers on the CUs the WIDE DP leaves idle, inputs
+    from the DP's epoch-tagged granules) against the pass after the DP: identical results, and
+    the concurrent pass did the items (so the granule hand-off, not the fallback, is tested)."""
+    rng = random.Random(23)
+    pairs = _pairs(rng, [(20000, 19000), (9000, 9500)], rate=0.2)
+    conc, st, sp = _run(pairs, "semiglobal", -1, -2, executes=3)
+    _check(oracle, "semiglobal", pairs, conc, -1, -2)
+    assert st["split"] == 1 and sp["tail_moves"] == 0 and sp["pairs_overflow"] == 0, sp
+    assert sp["items_beside_dp"] > 0, sp
+    monkeypatch.setenv("BG_SPLIT_CONC", "0")
+    post, _, sp0 = _run(pairs, "semiglobal", -1, -2)
+    assert sp0["items_beside_dp"] == 0 and sp0["tail_moves"] == 0, sp0
+    assert post == conc
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3, 4])
+def test_split_pipelined_two_dp_streams(oracle, depth):
+    """WIDE batches executed back to back: consecutive DPs alternate two HIP streams and run side
+    by side, each with its concurrent exit pass; every pipeline depth returns the reference's
+    answer for the last execute."""
+    from biogarden_amd import _native
+    rng = random.Random(100 + depth)
+    pairs = _pairs(rng, [(15000, 14000), (6000, 300)], rate=0.2)
+    h = _native.Handle(0)
+    try:
+        h.set_pipeline(depth)
+        h.prepare("semiglobal", pairs, _native.builtin_scoring(_native.BG_BLOSUM62), -1, -2)
+        for _ in range(5):
+            h.execute()
+        got = h.fetch()
+        sp = h.split_stats()
+    finally:
+        h.close()
+    _check(oracle, "semiglobal", pairs, got, -1, -2)
+    assert sp["tail_moves"] == 0, sp
