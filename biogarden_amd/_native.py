@@ -25,7 +25,7 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_aligner_set_call_dims", "bg_host_timing", "bg_last_hip_error",
            "bg_batch_export_compact", "bg_compact_expand", "bg_fasta_open",
            "bg_batch_prepare_table", "bg_fasta_next_batch",
-           "bg_fasta_close", "bg_split_stats"]
+           "bg_fasta_close", "bg_split_stats", "bg_split_conc_diag"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -116,6 +116,7 @@ def lib():
                                  ctypes.c_size_t]
     L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
     L.bg_split_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 5
+    L.bg_split_conc_diag.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
     L.bg_aligner_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
                                          ctypes.POINTER(ctypes.c_size_t)]
     L.bg_aligner_set_buffer_size.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t]
@@ -404,6 +405,13 @@ class Handle:
         check(lib().bg_split_stats(self._p, *[ctypes.byref(x) for x in v]))
         return dict(zip(("pairs_split", "strips_taken", "tail_moves", "pairs_overflow", "items_beside_dp"),
                         (x.value for x in v)))
+
+    def conc_diag(self):
+        """bg_split_conc_diag: the concurrent exit pass's abandon record (all zero: it ran to
+        the end of its items, or was not used)."""
+        v = (ctypes.c_uint32 * 6)()
+        check(lib().bg_split_conc_diag(self._p, v))
+        return dict(zip(("abandoned", "item", "input", "tag_seen", "epoch", "not_resident"), list(v)))
 
 
 def expand_compact(rec, pairs):

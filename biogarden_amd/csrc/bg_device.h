@@ -108,6 +108,11 @@ struct BgSplitArgs {
   const int32_t* order;
   uint32_t* counter;
   const uint32_t* resident;
+  // a worker that waits longer than waitTicks (s_memrealtime, 100 MHz) for one input abandons the
+  // concurrent pass (the pass after the DP does the remaining items): diag[0] = 1, [1] the item,
+  // [2] which input (1 top row, 2 checkpoint), [3] the tag lane 0 saw, [4] the epoch waited for
+  uint32_t* diag;
+  int32_t waitTicks;
   int32_t dpWgs;
   int32_t npairs, nitems;
   int32_t open, ext, mode, R, segc;

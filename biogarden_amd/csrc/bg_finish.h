@@ -27,6 +27,16 @@
 #ifndef BG_HELP_LONG
 #define BG_HELP_LONG 8
 #endif
+// the helpers' pauses: s_sleep, or (BG_FIN_NOSLEEP, s_wakeup diagnosis) busy s_nops, so that no
+// wave of the workgroup is ever in s_sleep
+#ifndef BG_FIN_NOSLEEP
+#define BG_FIN_NOSLEEP 0
+#endif
+#define help_pause(n)                                                   \
+  do {                                                                  \
+    if constexpr (BG_FIN_NOSLEEP) asm volatile("s_nop 7\n\ts_nop 7"); \
+    else __builtin_amdgcn_s_sleep(n);                                   \
+  } while (0)
 #include "bg_device.h"
 #include "bg_tag_common.h"
 
@@ -702,7 +712,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       int key = -1, zz = -1;
       if (lane == 0) {
         while (__hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
-          __builtin_amdgcn_s_sleep(1);
+          help_pause(1);
         const int req = __hip_atomic_load(&sh[33], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int kw = __hip_atomic_load(&sh[34], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int lw = __hip_atomic_load(&sh[35], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -790,8 +800,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         // idle: nothing to recompute ahead of the walk.  Each poll takes the lock and scans the
         // candidates on a SIMD the next execute's DP waves share; after BG_HELP_FAST idle polls
         // the helper polls BG_HELP_LONG x 64 cycles apart
-        if (idle < BG_HELP_FAST) { __builtin_amdgcn_s_sleep(8); ++idle; }
-        else __builtin_amdgcn_s_sleep(BG_HELP_LONG);
+        if (idle < BG_HELP_FAST) { help_pause(8); ++idle; }
+        else help_pause(BG_HELP_LONG);
         continue;
       }
       idle = 0;
@@ -970,10 +980,16 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
               __hip_atomic_store(&sh[35], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               __hip_atomic_store(&sh[33], key, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-#if BG_FIN_WAKEUP
+#if BG_FIN_WAKEUP == 1
             // experiment (round 2's failing variant, re-created for diagnosis): wake the sleeping
             // helpers of this workgroup right after posting the request
             asm volatile("s_wakeup" ::: "memory");
+#elif BG_FIN_WAKEUP == 2
+            asm volatile("s_nop 0" ::: "memory");             // the same statement, no wakeup
+#elif BG_FIN_WAKEUP == 3
+            asm volatile("s_wakeup");                         // the wakeup, no memory clobber
+#elif BG_FIN_WAKEUP == 4
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_wakeup" ::: "memory");   // after every access
 #endif
             const unsigned* me = &ckMap[ck_map_idx(reqS, reqB0)];
             // Forward progress: after kSelfPolls polls without a helper taking the request (all
@@ -1100,6 +1116,9 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       __builtin_amdgcn_s_setprio(0);
       if (lane == 0) { sh[4] = reqS; sh[5] = reqB0; sh[6] = done; sh[11] = crossed; }
       if (async && lane == 0) __hip_atomic_store(&sh[32], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#if BG_FIN_WAKEUP == 5
+      if (async) asm volatile("s_wakeup" ::: "memory");       // once, as the walk ends (diagnosis)
+#endif
     }
     __syncthreads();
     done = sh[6];

@@ -148,7 +148,7 @@ struct bg_aligner {
   hipStream_t stream4 = nullptr;   // WIDE batches at pipeline depth 4: every third one
   // WIDE batches: every other execute's DP.  A WIDE DP holds one CU per group workgroup (C3: 79 of
   // 256), so two executes' DPs run side by side on disjoint CUs (each waits for its own slot's
-  // previous traceback); created on first use, BG_ONE_DP_STREAM=1 keeps one
+  // previous traceback); created on first use (BG_TWO_DP_STREAMS=1)
   hipStream_t dps = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
   DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
@@ -201,7 +201,7 @@ struct bg_aligner {
   std::vector<int2> splitMap;
   std::vector<int32_t> splitBases;  // exit-pass item bases (np + 1), then resolve bases (np + 1),
                                     // then the items in estimated readiness order (concurrent pass)
-  int splitConc = 0;                // the exit pass runs beside the DP (BG_SPLIT_CONC=0: after it)
+  int splitConc = 0;                // the exit pass runs beside the DP (BG_SPLIT_CONC=1)
   DevBuf splitMapBuf, splitBaseBuf;
   int tagRow = 0;                  // tagged kernel: the code row staged whole in LDS
   std::vector<int> groupOf;        // caller pair -> workgroups (WIDE)
@@ -1001,7 +1001,7 @@ plan_again:
       // chunk c at about (3 s + c) chunk times (a strip starts ~3 chunks after the one above)
       {
         const char* ec = std::getenv("BG_SPLIT_CONC");
-        h->splitConc = !(ec && ec[0] == '0');
+        h->splitConc = (ec && ec[0] == '1') ? 1 : 0;
       }
       std::vector<std::pair<int64_t, int32_t>> keyed;
       keyed.reserve(h->splitItems);
@@ -1043,7 +1043,7 @@ plan_again:
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)) ||
         (h->split && S.split.cap < h->splitInts * 4 + 256 &&
          (!S.split.ensure(h->splitInts * 4 + 256) || hipMemset(S.split.p, 0, S.split.cap) != hipSuccess)) ||
-        (h->wide && !S.gprog.ensure(4 * ((size_t)h->progWords + 2))))
+        (h->wide && !S.gprog.ensure(4 * ((size_t)h->progWords + 8))))
       return BG_E_NOMEM;
     // WIDE checkpoint batches hand strip rows between workgroups as epoch-tagged granules: a
     // fresh arena is zeroed so that no stale tag (of another handle) can match an epoch
@@ -1199,8 +1199,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   Slot& S = h->slot[z];
   // the DP's stream: WIDE batches alternate two (see bg_aligner::dps)
   hipStream_t ds = h->stream;
-  if (h->wide && h->depth >= 2 && (h->execCount & 1) && !std::getenv("BG_ONE_DP_STREAM") &&
-      !std::getenv("BG_DP_TIMING")) {
+  const char* e2 = std::getenv("BG_TWO_DP_STREAMS");
+  if (h->wide && h->depth >= 2 && (h->execCount & 1) && e2 && e2[0] == '1' && !std::getenv("BG_DP_TIMING")) {
     if (!h->dps && hipStreamCreateWithFlags(&h->dps, hipStreamNonBlocking) != hipSuccess) h->dps = nullptr;
     if (h->dps) ds = h->dps;
   }
@@ -1233,7 +1233,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       A.dbg = h->dpDbg.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, ds));
     }
-    if (h->wide) BG_HIP(hipMemsetAsync(S.gprog.p, 0, 4 * ((size_t)h->progWords + 2), ds));
+    if (h->wide) BG_HIP(hipMemsetAsync(S.gprog.p, 0, 4 * ((size_t)h->progWords + 8), ds));
     if (h->split && h->splitConc) {
       if (!S.resetDone) BG_HIP(hipEventCreateWithFlags(&S.resetDone, hipEventDisableTiming));
       BG_HIP(hipEventRecord(S.resetDone, ds));
@@ -1317,6 +1317,12 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     X.resident = S.gprog.as<uint32_t>() + h->progWords;
     X.counter = S.gprog.as<uint32_t>() + h->progWords + 1;
     X.dpWgs = h->gridWgs;
+    X.diag = S.gprog.as<uint32_t>() + h->progWords + 2;
+    {
+      const char* ew = std::getenv("BG_SPLIT_WAIT_MS");
+      const long ms = ew ? std::atol(ew) : 500;
+      X.waitTicks = (int32_t)std::min<long>(std::max<long>(ms, 1) * 100000L, 0x7FFFFFFFL);
+    }
     if (h->splitConc && h->splitItems > 0) {
       X.conc = 1;
       void* cargs[] = {&X};
@@ -1618,6 +1624,17 @@ extern "C" int bg_split_stats(bg_aligner* h, uint64_t* pairs_split, uint64_t* st
     if (head[7] >= 0 && head[8] > 0) *strips_taken += (uint64_t)head[8];
     if (head[7] >= 0 && head[10] > 0) *tail_moves += (uint64_t)head[10];
   }
+  return BG_OK;
+}
+
+extern "C" int bg_split_conc_diag(bg_aligner* h, uint32_t* out6) {
+  if (!h || !out6) return BG_E_ARG;
+  for (int x = 0; x < 6; ++x) out6[x] = 0;
+  if (!h->split || !h->executed || !h->wide) return BG_OK;
+  const int rc = bg_synchronize(h);
+  if (rc) return rc;
+  const Slot& S = h->slot[h->lastSlot];
+  BG_HIP(hipMemcpy(out6, S.gprog.as<uint32_t>() + h->progWords + 2, 6 * 4, hipMemcpyDeviceToHost));
   return BG_OK;
 }
 

@@ -212,6 +212,30 @@ __device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
   const int32_t* topRow = A.bndM + topOff;
   const unsigned long long* topGran = A.gran + topOff;
   const int tclamp = n2 < NC * 64 - 1 ? n2 : NC * 64 - 1;
+  // CONC: a wait that outlasts A.waitTicks (or finds the pass abandoned by another wave)
+  // abandons the item and the pass; the pass after the DP then does what is left
+  bool dead = false;
+  unsigned long long t0 = 0;
+  int np = 0;
+  auto waited_out = [&](int which, unsigned long long tagv) {
+    if ((++np & 63) == 0) {
+      if (__hip_atomic_load(A.diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+      const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+      if (t0 == 0) t0 = now;
+      if (now - t0 > (unsigned long long)A.waitTicks) {
+        if (lane == 0) {
+          A.diag[1] = (uint32_t)item;
+          A.diag[2] = (uint32_t)which;
+          A.diag[3] = (uint32_t)(tagv >> 32);
+          A.diag[4] = A.epoch;
+          __threadfence();
+          __hip_atomic_store(A.diag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return true;
+      }
+    }
+    return false;
+  };
   // the top block of chunk c (columns c*64 + lane, clamped to n2)
   auto top_abs = [&](int c) {
     const int j = min(c * 64 + lane, tclamp);
@@ -219,7 +243,9 @@ __device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
       return topRow[j];
     } else {
       unsigned long long v = __hip_atomic_load(topGran + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t0 = 0;
       while (!__all((uint32_t)(v >> 32) == A.epoch)) {
+        if (waited_out(1, v)) { dead = true; break; }
         __builtin_amdgcn_s_sleep(8);
         v = __hip_atomic_load(topGran + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -257,7 +283,10 @@ __device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
 #pragma unroll
         for (int k = 0; k <= R; ++k) mine = mine && (uint32_t)(v[k] >> 32) == A.epoch;
         ok = __all(mine);
-        if (!ok) __builtin_amdgcn_s_sleep(8);
+        if (!ok) {
+          if (waited_out(2, v[0])) return;
+          __builtin_amdgcn_s_sleep(8);
+        }
       } while (!ok);
 #pragma unroll
       for (int k = 0; k < R; ++k) Yabs[k] = (int)(uint32_t)v[k];
@@ -270,6 +299,7 @@ __device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
   int* overflow = ar + L.head + (CONC ? 11 : 6);
   const int ovVal = CONC ? (int)A.epoch : 1;
   int mt = top_abs(c0);
+  if (dead) return;
   ExitStrip<R> S;
   int base = 0;
   // field value of an absolute M' (clampv for a clamped column-0 value)
@@ -323,6 +353,7 @@ __device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
     }
     bIn[lane] = fld(mt) | kT2 | (unsigned)(c * 64 + lane);
     if (c + 1 < c1) mt = top_abs(c + 1);                 // in flight while the chunk computes
+    if (dead) return;
 #pragma unroll
     for (int qq = 0; qq < 3; ++qq) {
       const int x = c * 64 - 64 + lane + 64 * qq;
@@ -391,7 +422,10 @@ __global__ __launch_bounds__(R >= 8 ? 512 : 1024) void bg_exit_conc_kernel(BgSpl
   const int w = uni(threadIdx.x >> 6);
   int polls = 0;
   while (__hip_atomic_load(A.resident, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (uint32_t)A.dpWgs) {
-    if (++polls > 4000) return;                          // ~0.25 ms: the DP has not started
+    if (++polls > 4000) {                                // ~2 ms: the DP has not started
+      if (threadIdx.x == 0) A.diag[5] = 1u;
+      return;
+    }
     __builtin_amdgcn_s_sleep(16);
   }
   int* wl = esm + w * exit_wave_ints<R>();
@@ -401,6 +435,7 @@ __global__ __launch_bounds__(R >= 8 ? 512 : 1024) void bg_exit_conc_kernel(BgSpl
     idx = uni(__shfl(idx, 0, 64));
     if (idx >= A.nitems) return;
     exit_item<R, true>(A, A.order[idx], lane, wl);
+    if (__hip_atomic_load(A.diag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;   // abandoned
   }
 }
 

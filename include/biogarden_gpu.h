@@ -170,6 +170,12 @@ int bg_get_stats(bg_aligner* h, bg_stats* out);
  * not split.  Waits for the handle's work.  The results never depend on it: a diagnostic. */
 int bg_split_stats(bg_aligner* h, uint64_t* pairs_split, uint64_t* strips_taken,
                    uint64_t* tail_moves, uint64_t* pairs_overflow, uint64_t* items_beside_dp);
+/* Diagnostics of the last execute's concurrent exit pass (BG_SPLIT_CONC=1), six words: [0] 1 if a
+ * worker waited longer than BG_SPLIT_WAIT_MS for an input and abandoned the pass (the pass after
+ * the DP then did the remaining items), [1] that item, [2] which input (1 the row above, 2 the
+ * segment's checkpoint), [3] the tag it saw, [4] the epoch it waited for, [5] 1 if the workers
+ * gave up waiting for the DP's workgroups to become resident.  Not a reference interface. */
+int bg_split_conc_diag(bg_aligner* h, uint32_t* out6);
 
 /* The reference aligner's scratch dims this handle models (SequenceAligner::buffer_size,
  * aligner.rs:30): 1024 x 1024 after bg_aligner_new (:44-55); every alignment call of a prepared

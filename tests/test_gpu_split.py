@@ -26,7 +26,7 @@ def _pairs(rng, shapes, rate=0.15):
     return out
 
 
-def _run(pairs, mode, a, b, R=0, scoring=None, env=None, monkeypatch=None, executes=1):
+def _run(pairs, mode, a, b, R=0, scoring=None, env=None, monkeypatch=None, executes=1, diag=None):
     from biogarden_amd import _native
     if env and monkeypatch is not None:
         for k, v in env.items():
@@ -40,6 +40,8 @@ def _run(pairs, mode, a, b, R=0, scoring=None, env=None, monkeypatch=None, execu
         for _ in range(executes):
             h.execute()
         got = h.fetch()
+        if diag is not None:
+            diag.update(h.conc_diag())
         return got, h.stats(), h.split_stats()
     finally:
         h.close()
@@ -126,9 +128,13 @@ def test_split_exit_pass_beside_dp(oracle, monkeypatch):
     the concurrent pass did the items (so the granule hand-off, not the fallback, is tested)."""
     rng = random.Random(23)
     pairs = _pairs(rng, [(20000, 19000), (9000, 9500)], rate=0.2)
-    conc, st, sp = _run(pairs, "semiglobal", -1, -2, executes=3)
+    monkeypatch.setenv("BG_SPLIT_CONC", "1")
+    dg = {}
+    conc, st, sp = _run(pairs, "semiglobal", -1, -2, executes=3, diag=dg)
+    print("conc diag", dg, "split", sp, flush=True)
     _check(oracle, "semiglobal", pairs, conc, -1, -2)
     assert st["split"] == 1 and sp["tail_moves"] == 0 and sp["pairs_overflow"] == 0, sp
+    assert dg["abandoned"] == 0 and dg["not_resident"] == 0, dg
     assert sp["items_beside_dp"] > 0, sp
     monkeypatch.setenv("BG_SPLIT_CONC", "0")
     post, _, sp0 = _run(pairs, "semiglobal", -1, -2)
@@ -137,11 +143,13 @@ def test_split_exit_pass_beside_dp(oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("depth", [1, 2, 3, 4])
-def test_split_pipelined_two_dp_streams(oracle, depth):
+def test_split_pipelined_two_dp_streams(oracle, monkeypatch, depth):
     """WIDE batches executed back to back: consecutive DPs alternate two HIP streams and run side
     by side, each with its concurrent exit pass; every pipeline depth returns the reference's
     answer for the last execute."""
     from biogarden_amd import _native
+    monkeypatch.setenv("BG_SPLIT_CONC", "1")
+    monkeypatch.setenv("BG_TWO_DP_STREAMS", "1")
     rng = random.Random(100 + depth)
     pairs = _pairs(rng, [(15000, 14000), (6000, 300)], rate=0.2)
     h = _native.Handle(0)
