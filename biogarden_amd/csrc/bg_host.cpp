@@ -201,7 +201,8 @@ struct bg_aligner {
   std::vector<int2> splitMap;
   std::vector<int32_t> splitBases;  // exit-pass item bases (np + 1), then resolve bases (np + 1),
                                     // then the items in estimated readiness order (concurrent pass)
-  int splitConc = 0;                // the exit pass runs beside the DP (BG_SPLIT_CONC=1)
+  int splitConc = 0;                // the exit pass beside the DP: 1 always (BG_SPLIT_CONC=1), 0 never
+                                    // (=0), 2 (unset) when no other execute's DP is in flight
   DevBuf splitMapBuf, splitBaseBuf;
   int tagRow = 0;                  // tagged kernel: the code row staged whole in LDS
   std::vector<int> groupOf;        // caller pair -> workgroups (WIDE)
@@ -1001,7 +1002,7 @@ plan_again:
       // chunk c at about (3 s + c) chunk times (a strip starts ~3 chunks after the one above)
       {
         const char* ec = std::getenv("BG_SPLIT_CONC");
-        h->splitConc = (ec && ec[0] == '1') ? 1 : 0;
+        h->splitConc = !ec ? 2 : ec[0] == '1' ? 1 : 0;
       }
       std::vector<std::pair<int64_t, int32_t>> keyed;
       keyed.reserve(h->splitItems);
@@ -1198,11 +1199,27 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   const int z = h->execCount % h->depth;
   Slot& S = h->slot[z];
   // the DP's stream: WIDE batches alternate two (see bg_aligner::dps)
+  // (C3, pipeline 3: 8.35 -> 4.82 ms per execute; BG_TWO_DP_STREAMS=0 keeps one).  Two WIDE DPs
+  // need 2 x gridWgs <= CU count workgroups resident (their strips spin on each other), and
+  // nothing else running waits for a DP, so they cannot hold each other's CUs.
   hipStream_t ds = h->stream;
   const char* e2 = std::getenv("BG_TWO_DP_STREAMS");
-  if (h->wide && h->depth >= 2 && (h->execCount & 1) && e2 && e2[0] == '1' && !std::getenv("BG_DP_TIMING")) {
+  if (h->wide && h->depth >= 2 && (h->execCount & 1) && !(e2 && e2[0] == '0') && 2 * h->gridWgs <= h->cus &&
+      !std::getenv("BG_DP_TIMING")) {
     if (!h->dps && hipStreamCreateWithFlags(&h->dps, hipStreamNonBlocking) != hipSuccess) h->dps = nullptr;
     if (h->dps) ds = h->dps;
+  }
+  // the exit pass beside the DP needs the CUs this DP leaves idle: in the automatic mode it runs
+  // only when no other execute's DP is still in flight (a lone alignment's wall, not a pipeline's
+  // throughput: a second DP wants those CUs)
+  bool conc = h->split && h->splitConc == 1;
+  if (h->split && h->splitConc == 2) {
+    conc = true;
+    if (h->execCount > 0) {
+      const hipError_t q = hipEventQuery(h->slot[h->lastSlot].dpDone);
+      if (q == hipErrorNotReady) conc = false;
+      else BG_HIP(q);
+    }
   }
   // the previous user of this slot must have finished reading its trace
   if (S.inflight) BG_HIP(hipStreamWaitEvent(ds, S.finDone, 0));
@@ -1234,7 +1251,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, ds));
     }
     if (h->wide) BG_HIP(hipMemsetAsync(S.gprog.p, 0, 4 * ((size_t)h->progWords + 8), ds));
-    if (h->split && h->splitConc) {
+    if (conc) {
       if (!S.resetDone) BG_HIP(hipEventCreateWithFlags(&S.resetDone, hipEventDisableTiming));
       BG_HIP(hipEventRecord(S.resetDone, ds));
     }
@@ -1246,7 +1263,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       A.wide_pace = ev ? std::atoi(ev) : 0;
     }
     A.gran = S.gran.as<unsigned long long>();
-    A.split = (h->split && h->splitConc) ? S.split.as<int32_t>() : nullptr;
+    A.split = conc ? S.split.as<int32_t>() : nullptr;
     A.segc = h->segc;
     A.resident = h->wide ? S.gprog.as<uint32_t>() + h->progWords : nullptr;
     A.trace = S.trace.as<uint32_t>();
@@ -1323,7 +1340,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       const long ms = ew ? std::atol(ew) : 500;
       X.waitTicks = (int32_t)std::min<long>(std::max<long>(ms, 1) * 100000L, 0x7FFFFFFFL);
     }
-    if (h->splitConc && h->splitItems > 0) {
+    if (conc && h->splitItems > 0) {
       X.conc = 1;
       void* cargs[] = {&X};
       void* cfn = bg_split_kernel_ptr(h->R, 3);

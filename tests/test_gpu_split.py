@@ -142,14 +142,15 @@ def test_split_exit_pass_beside_dp(oracle, monkeypatch):
     assert post == conc
 
 
-@pytest.mark.parametrize("depth", [1, 2, 3, 4])
-def test_split_pipelined_two_dp_streams(oracle, monkeypatch, depth):
+@pytest.mark.parametrize("depth,conc", [(1, None), (2, None), (3, None), (4, None), (3, "1"), (3, "0")])
+def test_split_pipelined_two_dp_streams(oracle, monkeypatch, depth, conc):
     """WIDE batches executed back to back: consecutive DPs alternate two HIP streams and run side
-    by side, each with its concurrent exit pass; every pipeline depth returns the reference's
-    answer for the last execute."""
+    by side (the default at depth >= 2), with the exit pass beside the DP automatic (only when no
+    other DP is in flight), forced on, or off; every pipeline depth returns the reference's answer
+    for the last execute."""
     from biogarden_amd import _native
-    monkeypatch.setenv("BG_SPLIT_CONC", "1")
-    monkeypatch.setenv("BG_TWO_DP_STREAMS", "1")
+    if conc is not None:
+        monkeypatch.setenv("BG_SPLIT_CONC", conc)
     rng = random.Random(100 + depth)
     pairs = _pairs(rng, [(15000, 14000), (6000, 300)], rate=0.2)
     h = _native.Handle(0)

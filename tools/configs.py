@@ -122,6 +122,7 @@ def main():
                               "gcups": round(st["cells"] / (walls[len(walls) // 2] * 1e-3) / 1e9, 2)}
             try:
                 line["split_stats"] = h.split_stats()
+                line["conc_diag"] = h.conc_diag()
             except Exception:                         # noqa: BLE001 (older library)
                 pass
         if args.check:
