@@ -195,6 +195,7 @@ struct BgDpArgs {
                              // granules, indexed like bndM (zeroed when allocated)
   uint32_t epoch;          // this execute's granule tag (never 0, never reused by the handle)
   int32_t wide_pace;       // WIDE: s_sleep(1)s strip 0 adds per 32 steps (slack for the chain)
+  int32_t prio;            // A/B (BG_DP_PRIO=1): the DP's waves issue at s_setprio 1
   // split traceback with the exit pass running beside the DP (bg_split.hip): the slot's split
   // arena (segment-start checkpoints as {value, epoch} granules, every strip's output row as
   // granules too), the exit pass's segment length, and the resident-workgroup counter
@@ -256,8 +257,9 @@ enum {
   BG_FIN_SCORE_ONLY = 2,   // end cell and score only, no traceback (analysis::seq::edit_distance)
   BG_FIN_LCS = 4,          // LCS tie rule in the recomputed trace; out2 receives the op codes
   BG_FIN_SYNC = 8,         // linear checkpoint traceback: recompute at barriers (BG_FIN_SYNC=1, A/B)
-  BG_FIN_SELFSERVE = 16    // asynchronous traceback: the walker recomputes every miss itself at
+  BG_FIN_SELFSERVE = 16,   // asynchronous traceback: the walker recomputes every miss itself at
                            // once (tests the forward-progress path; BG_FIN_SELFSERVE=1)
+  BG_FIN_NOPRIO = 32       // the walker keeps priority 0 (A/B of its s_setprio 3; BG_FIN_NOPRIO=1)
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

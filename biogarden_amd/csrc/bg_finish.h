@@ -268,6 +268,8 @@ __device__ void recompute_chunk_aff(const BgFinishArgs& F, const BgPair& P, int 
 template <int R, bool AFFINE, int MODE, bool CK = false>
 __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const u64 tK0 = __builtin_readcyclecounter();       // BG_FINISH_TIMING: the kernel's phases
+  const u64 tR0 = __builtin_amdgcn_s_memrealtime();
   constexpr int NW = AFFINE ? 4 : 2;
   constexpr int ROWS = BG_WAVE * R;
   constexpr int BLK_DW = R * BG_WAVE * NW;             // dwords per 32-step trace block
@@ -295,6 +297,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     for (int x = threadIdx.x; x < kCkMapEntries; x += blockDim.x) ckMap[x] = 0xFFFFFFFFu;
     __syncthreads();
   }
+  const u64 tK1 = __builtin_readcyclecounter();       // BG_FINISH_TIMING
 
   // split traceback phases (linear checkpoint traceback only, BgFinishArgs::phase): WALK runs one
   // strip of a pair per workgroup (F.splitMap), the others one pair per workgroup
@@ -397,7 +400,14 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       sh[0] = ei; sh[1] = ej; sh[2] = score; sh[3] = colcase; sh[9] = 0;
     }
   }
+  const u64 tR1 = __builtin_amdgcn_s_memrealtime();  // this wave at the end-cell barrier
   __syncthreads();
+  const u64 tK2 = __builtin_readcyclecounter();       // BG_FINISH_TIMING: end cell known
+  if (F.dbg && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 2) {
+    u64* d = F.dbg + (size_t)F.pairs[(ph == BG_PH_WALK) ? F.splitMap[blockIdx.x].x : blockIdx.x].index * 16;
+    d[11 + 2 * (threadIdx.x >> 6)] = tR0;
+    d[12 + 2 * (threadIdx.x >> 6)] = tR1;
+  }
   const int ei = uni(sh[0]), score = uni(sh[2]), colcase = uni(sh[3]);
   int ej = uni(sh[1]);
   if (ph == BG_PH_HEAD) {
@@ -821,7 +831,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     if (wid == 0) {
       // the walk is one latency-bound wave: first claim on the issue slots it shares with the
       // next execute's DP waves (two-stream pipeline)
-      __builtin_amdgcn_s_setprio(3);
+      if (!(F.flags & BG_FIN_NOPRIO)) __builtin_amdgcn_s_setprio(3);
       for (; !preDone;) {
         int dk = k0 - k, dl = l0 - l;
         if ((unsigned)dk >= 8u || (unsigned)dl >= 8u) { reanchor(k, l); dk = 0; dl = 0; }
@@ -1213,10 +1223,13 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     tMiss += __builtin_readcyclecounter() - tm0;
   }
   if (F.dbg && tid == 0) {
-    u64* d = F.dbg + (size_t)P.index * 8;
+    u64* d = F.dbg + (size_t)P.index * 16;
     d[0] = __builtin_readcyclecounter() - tWalk0;
     d[1] = tJump + tDec; d[2] = nJump + nDec; d[3] = tMiss; d[4] = nMiss; d[5] = (u64)ncore;
     d[6] = async ? (u64)sh[37] + nSelf : nRec;
+    d[7] = tWalk0 - tK0;                               // end cell, tail gaps, set-up
+    d[9] = tK1 - tK0;                                  // chunk map cleared
+    d[10] = tK2 - tK0;                                 // end cell known
   }
 
   // ---------------- semiglobal prefix gaps (:416-428); every wave knows k, l through sh
@@ -1243,14 +1256,23 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
 
   // ---------------- semiglobal prefix (:416-428) and tail columns: one residue run against gaps
   // each (prefix: s1[0, kstop) or s2[0, lstop); tail: s1[ei, n1) or s2[ej, n2))
-  for (int x = tid; x < npre; x += NT) {
-    ob[base + x] = colcase ? f.s1[x] : (uint8_t)'-';
-    ob2[base + x] = colcase ? (uint8_t)'-' : f.s2[x];
-  }
-  for (int x = tid; x < ntail; x += NT) {
-    ob[cap - ntail + x] = colcase ? f.s1[ei + x] : (uint8_t)'-';
-    ob2[cap - ntail + x] = colcase ? (uint8_t)'-' : f.s2[ej + x];
-  }
+  // (the residues of GB rounds are loaded before any of their stores: a load after a store to
+  // a buffer that may alias it waits for the load before the store, one round trip per column)
+  auto gap_run = [&](int dst, const uint8_t* src, int n) {
+    constexpr int GB = 8;
+    uint8_t* os = colcase ? ob + dst : ob2 + dst;      // the residues' side
+    uint8_t* og = colcase ? ob2 + dst : ob + dst;      // the gaps' side
+    for (int x0 = tid; x0 < n; x0 += GB * NT) {
+      uint8_t v[GB];
+#pragma unroll
+      for (int u = 0; u < GB; ++u) v[u] = (x0 + u * NT < n) ? src[x0 + u * NT] : (uint8_t)0;
+#pragma unroll
+      for (int u = 0; u < GB; ++u)
+        if (x0 + u * NT < n) { os[x0 + u * NT] = v[u]; og[x0 + u * NT] = (uint8_t)'-'; }
+    }
+  };
+  gap_run(base, colcase ? f.s1 : f.s2, npre);
+  gap_run(cap - ntail, colcase ? f.s1 + ei : f.s2 + ej, ntail);
 
   // ---------------- expand the walk's op codes into both strings (parallel scan over columns)
   const int i0 = kstop, j0 = lstop;                    // first residues the core consumes
@@ -1298,18 +1320,33 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     if (badop) printf("BGDBG pair %d: op code > 2 in the core (tid %d)\n", P.index, tid);
   }
 #endif
-  for (int x = lo; x < hi; ++x) {
-    const int op = ob[x];
+  // in rounds of EB columns: the ops, then the residues they consume, then the stores (the same
+  // aliasing rule as the gap runs: two round trips per round instead of two per column)
+  constexpr int EB = 8;
+  for (int x0 = lo; x0 < hi; x0 += EB) {
+    int opv[EB];
+    uint8_t c1v[EB], c2v[EB];
+#pragma unroll
+    for (int u = 0; u < EB; ++u) opv[u] = x0 + u < hi ? (int)ob[x0 + u] : 3;
+#pragma unroll
+    for (int u = 0; u < EB; ++u) {
+      const int op = opv[u];
 #if BG_FIN_DEBUG
-    if ((op != 2 && (p1 < 0 || p1 >= n1)) || (op != 1 && (p2 < 0 || p2 >= n2))) {
-      printf("BGDBG pair %d: expansion reads s1[%d] / s2[%d] of %d / %d (op %d)\n", P.index, p1, p2, n1, n2, op);
-      break;
-    }
+      if (op != 3 && ((op != 2 && (p1 < 0 || p1 >= n1)) || (op != 1 && (p2 < 0 || p2 >= n2))))
+        printf("BGDBG pair %d: expansion reads s1[%d] / s2[%d] of %d / %d (op %d)\n", P.index, p1, p2, n1, n2, op);
 #endif
-    const uint8_t ch1 = op != 2 ? f.s1[p1++] : (uint8_t)'-';
-    const uint8_t ch2 = op != 1 ? f.s2[p2++] : (uint8_t)'-';
-    ob[x] = ch1;
-    ob2[x] = (F.flags & BG_FIN_LCS) ? (uint8_t)op : ch2;   // LCS: the caller keeps op-0 columns
+      const bool t1 = op == 0 || op == 1, t2 = op == 0 || op == 2;
+      c1v[u] = t1 ? f.s1[p1] : (uint8_t)'-';
+      c2v[u] = t2 ? f.s2[p2] : (uint8_t)'-';
+      p1 += t1;
+      p2 += t2;
+    }
+#pragma unroll
+    for (int u = 0; u < EB; ++u)
+      if (x0 + u < hi) {
+        ob[x0 + u] = c1v[u];
+        ob2[x0 + u] = (F.flags & BG_FIN_LCS) ? (uint8_t)opv[u] : c2v[u];   // LCS: the caller keeps op-0 columns
+      }
   }
   if (tid == 0) {
     BgResult res;
@@ -1324,6 +1361,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     res.npre = (uint32_t)npre;
     res.ntail = (uint32_t)ntail;
     F.results[P.index] = res;
+    if (F.dbg) F.dbg[(size_t)P.index * 16 + 8] = __builtin_readcyclecounter() - tK0;   // whole kernel
   }
 }
 

@@ -1261,6 +1261,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     {
       const char* ev = std::getenv("BG_WIDE_PACE");
       A.wide_pace = ev ? std::atoi(ev) : 0;
+      A.prio = std::getenv("BG_DP_PRIO") ? 1 : 0;
     }
     A.gran = S.gran.as<unsigned long long>();
     A.split = conc ? S.split.as<int32_t>() : nullptr;
@@ -1390,9 +1391,13 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.splitMap = h->splitMapBuf.as<int2>();
     if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;
     if (std::getenv("BG_FIN_SELFSERVE")) F.flags |= BG_FIN_SELFSERVE;
-    if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(64 * (np + 1))) {
+    // the walker's priority 3 costs a many-pair batch's DP (the metric: 10 390 -> 10 530 GCUPS
+    // without it, tools/r04/prio_ab.sh); a WIDE batch's walks are its latency (BG_FIN_PRIO=1 /
+    // BG_FIN_NOPRIO=1 force either)
+    if (std::getenv("BG_FIN_NOPRIO") || (!h->wide && !std::getenv("BG_FIN_PRIO"))) F.flags |= BG_FIN_NOPRIO;
+    if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(128 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
-      BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 64 * np, fs));
+      BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 128 * np, fs));
     }
     void* args[] = {&F};
     int fnw = 4, fns = 0;
@@ -1504,13 +1509,24 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
     }
   }
   if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.p && np) {
-    std::vector<unsigned long long> d(8 * np);
-    BG_HIP(hipMemcpy(d.data(), h->dbgBuf.p, 64 * np, hipMemcpyDeviceToHost));
-    double s[7] = {0, 0, 0, 0, 0, 0, 0};
+    std::vector<unsigned long long> d(16 * np);
+    BG_HIP(hipMemcpy(d.data(), h->dbgBuf.p, 128 * np, hipMemcpyDeviceToHost));
+    double s[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     for (size_t p = 0; p < np; ++p)
-      for (int x = 0; x < 7; ++x) s[x] += (double)d[8 * p + x];
-    std::fprintf(stderr, "finish timing (per pair avg, cycles): walk %.0f  jump %.0f (n %.1f)  miss %.0f (n %.1f)  ops %.0f  chunks recomputed %.1f\n",
-                 s[0] / np, s[1] / np, s[2] / np, s[3] / np, s[4] / np, s[5] / np, s[6] / np);
+      for (int x = 0; x < 11; ++x) s[x] += (double)d[16 * p + x];
+    std::fprintf(stderr, "finish timing: before walk: map cleared at %.0f, end cell at %.0f\n", s[9] / np, s[10] / np);
+    double w0 = 0, w1 = 0, l01 = 0;
+    for (size_t p = 0; p < np; ++p) {
+      const auto* q = &d[16 * p];
+      w0 += (double)(q[12] - q[11]);
+      if (q[13]) { w1 += (double)(q[14] - q[13]); l01 += (double)q[13] - (double)q[11]; }
+    }
+    std::fprintf(stderr, "finish timing (us): wave 0 entry -> end-cell barrier %.2f, wave 1 %.2f, wave 1 entry after wave 0 by %.2f\n",
+                 w0 / np * 0.01, w1 / np * 0.01, l01 / np * 0.01);
+    std::fprintf(stderr, "finish timing (per pair avg, cycles): kernel %.0f = before walk %.0f + walk %.0f + after %.0f;"
+                 "  walk: jump %.0f (n %.1f)  miss %.0f (n %.1f)  ops %.0f  chunks recomputed %.1f\n",
+                 s[8] / np, s[7] / np, s[0] / np, (s[8] - s[7] - s[0]) / np,
+                 s[1] / np, s[2] / np, s[3] / np, s[4] / np, s[5] / np, s[6] / np);
   }
   h->hres.resize(np);
   uint64_t ob = 0;

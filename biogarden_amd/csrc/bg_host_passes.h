@@ -312,31 +312,43 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
   for (size_t p = 0; p < np; ++p) {
     const bg_compact_hdr& h = hd[p];
     const uint64_t ncore = (uint64_t)h.len - h.npre - h.ntail;
+    // BG_COMPACT_DEBUG: name the record that fails a check (stderr)
+    auto bad = [&](int why) {
+      if (std::getenv("BG_COMPACT_DEBUG"))
+        std::fprintf(stderr, "compact_expand: pair %zu check %d: status %u len %u npre %u ntail %u start %u %u end %u %u n %zu %zu\n",
+                     p, why, (unsigned)h.status, (unsigned)h.len, (unsigned)h.npre, (unsigned)h.ntail,
+                     (unsigned)h.start1, (unsigned)h.start2, (unsigned)h.end_i, (unsigned)h.end_j, n1[p], n2[p]);
+      return BG_E_ARG;
+    };
     if ((uint64_t)h.npre + h.ntail > h.len || h.len > n1[p] + n2[p] || h.ops_off + (ncore + 3) / 4 > opsBytes ||
         h.start1 > n1[p] || h.start2 > n2[p] || h.end_i > n1[p] || h.end_j > n2[p] ||
         (n1[p] && !s1[p]) || (n2[p] && !s2[p]))
-      return BG_E_ARG;
+      return bad(1);
     // the core consumes exactly s1[start1, end_i) and s2[start2, end_j)
     uint64_t c1 = 0, c2 = 0;
     for (uint64_t x = 0; x < ncore; ++x) {
       const int op = (ops[h.ops_off + x / 4] >> (2 * (x % 4))) & 3;
-      if (op == 3) return BG_E_ARG;
+      if (op == 3) return bad(2);
       c1 += op != 2;
       c2 += op != 1;
     }
-    if (h.start1 + c1 != h.end_i || h.start2 + c2 != h.end_j) return BG_E_ARG;
+    if (h.start1 + c1 != h.end_i || h.start2 + c2 != h.end_j) return bad(3);
     // the reference's semiglobal assembly (aligner.rs:389-428): the tail gap columns run from the
     // end cell to the last row / column, and a walk that returned (status 0) is preceded by the
     // prefix of the sequence it stopped in, exactly up to its start cell (row case: s2[0, start2),
     // column case: s1[0, start1)); the other modes have neither
     const bool colcase = h.end_i < n1[p];
     if (!semi) {
-      if (h.npre || h.ntail) return BG_E_ARG;
+      if (h.npre || h.ntail) return bad(4);
     } else {
       const uint64_t tail = colcase ? n1[p] - h.end_i : n2[p] - h.end_j;
       const uint64_t pre = colcase ? h.start1 : h.start2;
-      if (h.status == 0 ? (h.npre != pre || h.ntail != tail) : (h.npre != 0 || (h.ntail && h.ntail != tail)))
-        return BG_E_ARG;
+      // status 4 is either a walk that stopped at an index underflow (no prefix) or a complete
+      // walk the host flagged BG_REF_DIVERGENT (bg_ref_divergent: prefix and tail as status 0)
+      const bool whole = h.npre == pre && h.ntail == tail;
+      const bool stopped = h.npre == 0 && (h.ntail == 0 || h.ntail == tail);
+      if (h.status == 0 ? !whole : h.status == BG_REF_DIVERGENT ? !(whole || stopped) : !stopped)
+        return bad(5);
     }
   }
   par_ranges(np, [&](size_t p) -> uint64_t { return 2ull * hd[p].len + 64; }, [&](size_t lo, size_t hi) {

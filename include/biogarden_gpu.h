@@ -192,8 +192,9 @@ int bg_aligner_set_buffer_size(bg_aligner* h, size_t rows, size_t cols);
  * resize rule over the whole batch in caller order, so every rank judges status BG_REF_DIVERGENT
  * against the history one reference aligner fed the whole batch would have).  rows / cols hold
  * npairs entries; the next bg_batch_prepare / bg_batch_prepare_table must have exactly npairs
- * pairs (else it returns BG_E_ARG) and consumes them; afterwards the handle's dims are what the
- * last pair's call leaves.  npairs = 0 or NULL arrays clear a pending set. */
+ * pairs (else it returns BG_E_ARG and leaves them pending) and a successful prepare consumes
+ * them; afterwards the handle's dims are what the last pair's call leaves.  npairs = 0 or NULL
+ * arrays clear a pending set. */
 int bg_aligner_set_call_dims(bg_aligner* h, size_t npairs, const uint64_t* rows, const uint64_t* cols);
 
 /* Kernel timing over a region of executes (HIP events recorded on the handle's stream around

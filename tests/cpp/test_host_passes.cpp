@@ -200,8 +200,10 @@ int main() {
       const bool colcase = i < n1;
       // semiglobal assembly (aligner.rs:389-428): the tail runs to the last row / column; a
       // returned walk (status 0) has the prefix up to its start cell; other modes have neither
-      h.npre = (uint32_t)(semi && h.status == 0 ? (colcase ? s1 : s2) : 0);
-      h.ntail = (uint32_t)(semi && (h.status == 0 || rng() % 2) ? (colcase ? n1 - i : n2 - j) : 0);
+      // (status 4 is also a complete walk the host flagged BG_REF_DIVERGENT: prefix and tail too)
+      const bool whole = h.status == 0 || (h.status == BG_REF_DIVERGENT && rng() % 2);
+      h.npre = (uint32_t)(semi && whole ? (colcase ? s1 : s2) : 0);
+      h.ntail = (uint32_t)(semi && (whole || rng() % 2) ? (colcase ? n1 - i : n2 - j) : 0);
       h.len = (uint32_t)(h.npre + core.size() + h.ntail);
       h.ops_off = ops.size();
       for (size_t q = 0; q < core.size(); q += 4) {
@@ -266,8 +268,11 @@ int main() {
         bad = rec;
         std::memcpy(&h0, bad.data() + 32, sizeof(h0));
         if (kind == 0) {
-          if (!semi || h0.status != 0) { h0.npre += 1; }
-          else { h0.npre = h0.npre ? h0.npre - 1 : 1; }
+          const bool cc0 = h0.end_i < n1[0];
+          const uint32_t pre0 = (uint32_t)(cc0 ? h0.start1 : h0.start2);
+          if (!semi || (h0.status != 0 && h0.status != BG_REF_DIVERGENT)) h0.npre += 1;
+          else if (h0.status == 0) h0.npre = h0.npre ? h0.npre - 1 : 1;
+          else h0.npre = pre0 + 1;                           // neither 0 nor the prefix
         } else {
           const bool cc0 = h0.end_i < n1[0];
           h0.ntail = (uint32_t)((cc0 ? n1[0] - h0.end_i : n2[0] - h0.end_j) + 1);   // past the end

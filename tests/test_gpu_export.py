@@ -128,7 +128,9 @@ def test_call_dims_mismatch_is_rejected():
         h.set_call_dims([(1024, 1024)] * 3)
         with pytest.raises(RuntimeError):
             h.prepare("global", _pairs(1, n=2), _native.builtin_scoring(_native.BG_BLOSUM62), -11, -1)
-        # consumed: the next prepare runs from the handle's own history
+        # a rejected prepare leaves them pending: the batch they were set for still takes them
+        # (and consumes them), after which the handle runs from its own history again
+        h.prepare("global", _pairs(1, n=3), _native.builtin_scoring(_native.BG_BLOSUM62), -11, -1)
         h.prepare("global", _pairs(1, n=2), _native.builtin_scoring(_native.BG_BLOSUM62), -11, -1)
     finally:
         h.close()
