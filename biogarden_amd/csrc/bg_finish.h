@@ -444,6 +444,14 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     ntw = 0;
   }
   const int kStart = k, lStart = l;
+  // an op index outside the walk's capacity (never expected: every move decrements k or l) is
+  // dropped and the pair reported BG_INTERNAL instead of written out of bounds
+  bool wild = false;
+  auto put_op = [&](int at, int op) {
+    const int idx = capw - 1 - at;
+    if ((unsigned)idx < (unsigned)capw) obw[idx] = (uint8_t)op;
+    else wild = true;
+  };
   int k0 = -1000000, l0 = -1000000;                  // neighbourhood anchor (invalid)
   int codes = 0;
   // Transition table of backtrack (aligner.rs:520-586), per state, indexed by the 4-bit cell code
@@ -874,7 +882,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             if (lane == 0 && ntw + ncore + nops > capw)
               printf("BGDBG pair %d: jumper writes op %d of cap %d at (%d, %d)\n", P.index, ntw + ncore + nops, capw, k, l);
 #endif
-            if (lane < nops) obw[capw - 1 - (ntw + ncore + lane)] = (uint8_t)opx;
+            if (lane < nops) put_op(ntw + ncore + lane, opx);
             ncore += nops;
             k -= Pn >> 3;
             l -= Pn & 7;
@@ -905,7 +913,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             const u64 TX = Tm | ballot(cl & 4);        // a run up stops here (x_trace 'M' or end)
             const u64 TY = Tm | ballot(cl & 8);
             auto emit = [&](int pos, int n, int op) {  // ops pos .. pos+n-1 of this walk
-              for (int q = 0; q < n; ++q) obw[capw - 1 - (ntw + pos + q)] = (uint8_t)op;
+              for (int q = 0; q < n; ++q) put_op(ntw + pos + q, op);
             };
             // the run the walk is in at the anchor (state X / Y), resolved in scalar
             int s0 = 0;
@@ -1119,12 +1127,13 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         l -= (0xA >> mv) & 1;
         state = e & 3;
         if (mv) {
-          if (lane == 0) obw[capw - 1 - (ntw + ncore)] = (uint8_t)(mv - 1);
+          if (lane == 0) put_op(ntw + ncore, mv - 1);
           ++ncore;
         }
       }
       __builtin_amdgcn_s_setprio(0);
       if (lane == 0) { sh[4] = reqS; sh[5] = reqB0; sh[6] = done; sh[11] = crossed; }
+      if (ballot(wild) && lane == 0) sh[9] = 5;                // BG_INTERNAL: see put_op
       if (async && lane == 0) __hip_atomic_store(&sh[32], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #if BG_FIN_WAKEUP == 5
       if (async) asm volatile("s_wakeup" ::: "memory");       // once, as the walk ends (diagnosis)
