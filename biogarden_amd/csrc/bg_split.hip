@@ -478,26 +478,66 @@ __global__ __launch_bounds__(256) void bg_exit_resolve_kernel(BgSplitArgs A) {
   int* prev = fa;
   int* cur = fb;
   for (int x = tid; x < F; x += blockDim.x) { prev[x] = fr[x]; fs[x] = fr[x]; }
-  __syncthreads();
-  for (int g = 1; g + 1 < L.G; ++g) {
-    for (int x = tid; x < F; x += blockDim.x) {
-      const int raw = fr[(size_t)g * F + x];
-      const int v = raw >= kSym ? prev[raw - kSym] : raw;
-      cur[x] = v;
-      fs[(size_t)g * F + x] = v;
+  // The segments form a chain (segment g's symbols point into g - 1's resolved frontier), but
+  // their raw frontiers do not depend on it: each thread keeps the raw values of the next D
+  // segments in flight, so a link costs an LDS lookup and a barrier, not an HBM round trip.
+  // (The 256 threads cover F <= 704 entries in QF passes.)
+  constexpr int D = 8, QF = (F + 255) / 256;
+  int raw[D][QF];
+  auto fetch = [&](int g, int (&r)[QF]) {
+#pragma unroll
+    for (int q = 0; q < QF; ++q) {
+      const int x = tid + 256 * q;
+      r[q] = (g + 1 < L.G && x < F) ? fr[(size_t)g * F + x] : 0;
     }
-    __syncthreads();
-    int* t = prev; prev = cur; cur = t;
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d) fetch(1 + d, raw[d]);
+  __syncthreads();
+  for (int g0 = 1; g0 + 1 < L.G; g0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int g = g0 + d;
+      if (g + 1 >= L.G) break;                           // block-uniform
+#pragma unroll
+      for (int q = 0; q < QF; ++q) {
+        const int x = tid + 256 * q;
+        if (x < F) {
+          const int rv = raw[d][q];
+          const int v = rv >= kSym ? prev[rv - kSym] : rv;
+          cur[x] = v;
+          fs[(size_t)g * F + x] = v;
+        }
+      }
+      fetch(g + D, raw[d]);                              // this slot's next segment
+      __syncthreads();
+      int* t = prev; prev = cur; cur = t;
+    }
   }
   __threadfence_block();
   __syncthreads();
   if (s < sStar) {
+    // rounds of EBK columns: the raw exits, then the lookups they need, then the stores (a load
+    // after a store to a possibly aliasing buffer would wait a round trip per column)
+    constexpr int EBK = 8;
     int32_t* eb = ar + L.ebot + (size_t)s * (n2 + 1);
-    for (int j = tid; j <= n2; j += blockDim.x) {
-      const int raw = eb[j];
-      if (raw >= kSym) {
+    for (int j0 = tid; j0 <= n2; j0 += EBK * 256) {
+      int rv[EBK], nv[EBK];
+#pragma unroll
+      for (int u = 0; u < EBK; ++u) {
+        const int j = j0 + 256 * u;
+        rv[u] = j <= n2 ? eb[j] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < EBK; ++u) {
+        const int j = j0 + 256 * u;
         const int seg = ((j + 63) >> 6) / A.segc;       // lane 63 is at column j at step j + 63
-        eb[j] = seg >= 1 ? fs[(size_t)(seg - 1) * F + (raw - kSym)] : -1;
+        nv[u] = rv[u] < kSym ? rv[u] : (seg >= 1 ? fs[(size_t)(seg - 1) * F + (rv[u] - kSym)] : -1);
+      }
+#pragma unroll
+      for (int u = 0; u < EBK; ++u) {
+        const int j = j0 + 256 * u;
+        if (j <= n2 && rv[u] >= kSym) eb[j] = nv[u];
       }
     }
   }
