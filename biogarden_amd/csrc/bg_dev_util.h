@@ -76,6 +76,20 @@ __device__ __forceinline__ int load_agent(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// End-cell keys (the reference's first / last and > / >= rules as one u64 max): the value biased
+// to unsigned in the high word, the index rule in the low word
+__device__ __forceinline__ unsigned key_bias(int v) { return (unsigned)v ^ 0x80000000u; }
+__device__ __forceinline__ u64 wave_umax64(u64 v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const unsigned lo = __shfl_xor((unsigned)v, o, 64);
+    const unsigned hi = __shfl_xor((unsigned)(v >> 32), o, 64);
+    const u64 other = ((u64)hi << 32) | lo;
+    v = other > v ? other : v;
+  }
+  return v;
+}
+
 // Row 0 / column 0 initialisation per mode (aligner.rs:96-104, 163, 233-237, 299, 360).
 __device__ __forceinline__ int row0_M(int mode, int j, int a, int b) {
   if (j == 0) return 0;

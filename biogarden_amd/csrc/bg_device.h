@@ -119,6 +119,10 @@ struct BgSplitArgs {
   int32_t margin;          // headroom below a chunk's smallest input: clampv + max(0, max S - 2a) + 1
   int32_t clampv;          // max(0, -(min S - 2a)): field value of a clamped column-0 value
   int32_t grow;            // 65 * max(0, max S - 2a): growth of a value inside one chunk
+  // end-cell keys of the split pairs, folded by many workgroups (bg_endkey_kernel) before the
+  // traceback's HEAD phase: [2p] column n2 (bias(M) << 32 | ~i), [2p + 1] row n1 (| j)
+  unsigned long long* endKeys;
+  const int32_t* aux;      // the slot's aux arena (column n2: M(i, n2) at aux_off + i)
 };
 
 // Would the reference SequenceAligner, whose scratch is rows x cols when this call starts
@@ -205,6 +209,7 @@ struct BgDpArgs {
 };
 
 struct BgFinishArgs {
+  const unsigned long long* keys;   // split HEAD: bg_endkey_kernel's keys (BgSplitArgs::endKeys), or nullptr
   const BgPair* pairs;
   const uint8_t* seq1;     // raw bytes (the aligned strings are built from them)
   const uint8_t* seq2;

@@ -342,7 +342,19 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   } else {
     u64 ka = 0, kb = 0;
     const int32_t* rowbest = f.lastcol + (n1 + 1);
-    if (mode == BGK_LOCAL) {
+    // split HEAD: the keys of i, j >= 1 were folded by bg_endkey_kernel; the border cells here
+    const bool folded = ph == BG_PH_HEAD && F.keys != nullptr && n1 > 0 && n2 > 0 && P.nstrips > 0 &&
+                        (mode == BGK_SEMIGLOBAL || mode == BGK_OVERLAP || mode == BGK_FITTING);
+    if (folded) {
+      if (tid == 0) {
+        ka = F.keys[2 * (size_t)pidx];
+        kb = F.keys[2 * (size_t)pidx + 1];
+        const u64 ka0 = ((u64)bias(lastcolM(f, 0)) << 32) | 0xFFFFFFFFu;
+        const u64 kb0 = (u64)bias(lastrowM(f, 0)) << 32;
+        ka = ka0 > ka ? ka0 : ka;
+        kb = kb0 > kb ? kb0 : kb;
+      }
+    } else if (mode == BGK_LOCAL) {
       // first row-major cell with the strict maximum; (0,0) with 0 when nothing is positive
       if (n2 > 0) {
 #pragma unroll 4
@@ -358,7 +370,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         ka = kk > ka ? kk : ka;
       }
     }
-    if (mode == BGK_OVERLAP || mode == BGK_SEMIGLOBAL) {
+    if (!folded && (mode == BGK_OVERLAP || mode == BGK_SEMIGLOBAL)) {
 #pragma unroll 4
       for (int j = tid; j <= n2; j += NT) {          // last row, last max (:308, :369)
         const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
@@ -676,12 +688,33 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       __syncthreads();
       // copy: one wave per strip; the strip's ops sit at the end of its scratch in the slot's order
       const uint8_t* scr = reinterpret_cast<const uint8_t*>(spl) + SL.ops;
-      for (int x = wid; x < nt; x += NWV) {
-        const int s = sStar - x;
-        const int n = hd[s].nops;
-        const uint8_t* src = scr + (size_t)s * SL.capS + (SL.capS - n);
-        uint8_t* dst = ob + (cap - ntail - preArr[x] - n);
-        for (int y = lane; y < n; y += 64) dst[y] = src[y];
+      // (a strip's op count from the LDS prefix sums; its bytes loaded in rounds of CB per lane
+      // before any is stored: one HBM round trip per strip rather than per 64 bytes)
+      // (two strips per wave and round: both strips' loads go out before either's stores)
+      constexpr int CB = 8;
+      for (int x = wid; x < nt; x += 2 * NWV) {
+        const int xb = x + NWV;
+        const int na = (x + 1 < nt ? preArr[x + 1] : total) - preArr[x];
+        const int nb = xb < nt ? (xb + 1 < nt ? preArr[xb + 1] : total) - preArr[xb] : 0;
+        const uint8_t* srcA = scr + (size_t)(sStar - x) * SL.capS + (SL.capS - na);
+        const uint8_t* srcB = scr + (size_t)(sStar - (xb < nt ? xb : x)) * SL.capS + (SL.capS - nb);
+        uint8_t* dstA = ob + (cap - ntail - preArr[x] - na);
+        uint8_t* dstB = ob + (cap - ntail - (xb < nt ? preArr[xb] : 0) - nb);
+        for (int y0 = lane; y0 < na || y0 < nb; y0 += CB * 64) {
+          uint8_t va[CB], vb[CB];
+#pragma unroll
+          for (int u = 0; u < CB; ++u) {
+            const int y = y0 + 64 * u;
+            va[u] = y < na ? srcA[y] : (uint8_t)0;
+            vb[u] = y < nb ? srcB[y] : (uint8_t)0;
+          }
+#pragma unroll
+          for (int u = 0; u < CB; ++u) {
+            const int y = y0 + 64 * u;
+            if (y < na) dstA[y] = va[u];
+            if (y < nb) dstB[y] = vb[u];
+          }
+        }
       }
       ncore = total;
       ffOps = total;
@@ -1291,17 +1324,30 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   const int lo = cbase + tid * seg < cend ? cbase + tid * seg : cend;
   const int hi = lo + seg < cend ? lo + seg : cend;
   int c1 = 0, c2 = 0;
-  for (int x = lo; x < hi; ++x) { const int op = ob[x]; c1 += op != 2; c2 += op != 1; }
+  for (int x0 = lo; x0 < hi; x0 += 8) {               // 8 loads in flight per round
+    int opv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) opv[u] = x0 + u < hi ? (int)ob[x0 + u] : 3;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { c1 += opv[u] == 0 || opv[u] == 1; c2 += opv[u] == 0 || opv[u] == 2; }
+  }
   // the core's ops, 2 bits per column (the compact export's payload, bg_batch_export_compact),
   // before the expansion below overwrites them with residues
   if (F.ops) {
     uint8_t* po = F.ops + P.ops_off;
-    for (int g = tid; g < (ncore + 3) / 4; g += NT) {
-      unsigned v = 0;
+    const int ng = (ncore + 3) / 4;
+    for (int g0 = tid; g0 < ng; g0 += 4 * NT) {        // 4 packed bytes per thread per round
+      unsigned v[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (4 * g + q < ncore) v |= (unsigned)(ob[cbase + 4 * g + q] & 3) << (2 * q);
-      po[g] = (uint8_t)v;
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int g = g0 + r * NT;
+          if (g < ng && 4 * g + q < ncore) v[r] |= (unsigned)(ob[cbase + 4 * g + q] & 3) << (2 * q);
+        }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (g0 + r * NT < ng) po[g0 + r * NT] = (uint8_t)v[r];
     }
   }
   scan[tid] = c1;
@@ -1331,7 +1377,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
 #endif
   // in rounds of EB columns: the ops, then the residues they consume, then the stores (the same
   // aliasing rule as the gap runs: two round trips per round instead of two per column)
-  constexpr int EB = 8;
+  constexpr int EB = 16;
   for (int x0 = lo; x0 < hi; x0 += EB) {
     int opv[EB];
     uint8_t c1v[EB], c2v[EB];

@@ -33,6 +33,8 @@ extern "C" void* bg_dp_kernel_lcs_ptr(int R, int dna);
 extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt);
 extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode);
 extern "C" void* bg_split_kernel_ptr(int R, int which);
+extern "C" void* bg_endkey_kernel_ptr(void);
+extern "C" int bg_endkey_blocks(void);
 extern "C" int bg_exit_lds_bytes(int R);
 extern "C" int bg_exit_conc_lds_bytes(int R);
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
@@ -134,6 +136,7 @@ struct PhaseTimer {
 // DP kernel of execute k+1 (stream) fills the other slot's trace.
 struct Slot {
   DevBuf trace, bndM, bndX, aux, out1, out2, results, ops, gran, split, gprog;
+  DevBuf keys;                      // split pairs: bg_endkey_kernel's end-cell keys (2 u64 per pair)
   hipEvent_t dpDone = nullptr, finDone = nullptr;
   hipEvent_t resetDone = nullptr;   // the DP's progress words zeroed (the concurrent exit pass waits)
   bool inflight = false;
@@ -328,7 +331,7 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
   for (Slot& S : h->slot) {
     for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops, &S.gran, &S.split,
-                      &S.gprog})
+                      &S.gprog, &S.keys})
       d->release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
     if (S.finDone) (void)hipEventDestroy(S.finDone);
@@ -1042,6 +1045,7 @@ plan_again:
         !S.bndX.ensure((h->affine || h->ack) ? bo * 4 + 256 : 256) || !S.aux.ensure(ao * 4 + 256) ||
         !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) || !S.ops.ensure(po + 16) ||
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)) ||
+        (h->split && !S.keys.ensure(16 * (h->plan.size() + 1))) ||
         (h->split && S.split.cap < h->splitInts * 4 + 256 &&
          (!S.split.ensure(h->splitInts * 4 + 256) || hipMemset(S.split.p, 0, S.split.cap) != hipSuccess)) ||
         (h->wide && !S.gprog.ensure(4 * ((size_t)h->progWords + 8))))
@@ -1335,6 +1339,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     X.resident = S.gprog.as<uint32_t>() + h->progWords;
     X.counter = S.gprog.as<uint32_t>() + h->progWords + 1;
     X.dpWgs = h->gridWgs;
+    X.endKeys = S.keys.as<unsigned long long>();
+    X.aux = S.aux.as<int32_t>();
     X.diag = S.gprog.as<uint32_t>() + h->progWords + 2;
     {
       const char* ew = std::getenv("BG_SPLIT_WAIT_MS");
@@ -1359,6 +1365,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   BG_HIP(hipEventRecord(e[2], fs));
   if (np) {
     BgFinishArgs F;
+    F.keys = nullptr;
     F.pairs = h->pairs.as<BgPair>();
     F.seq1 = h->seq1.as<uint8_t>();
     F.seq2 = h->seq2.as<uint8_t>();
@@ -1428,6 +1435,10 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
         // split traceback: end cell -> exit pass (the items the pass beside the DP
         // did not do) -> per-strip resolve -> chain -> the strips' walks in parallel -> stitch
         void* xargs[] = {&X};
+        // the end-cell keys folded by many workgroups per pair, then HEAD reads them
+        BG_HIP(hipMemsetAsync(S.keys.p, 0, 16 * (size_t)np, fs));
+        BG_HIP(hipLaunchKernel(bg_endkey_kernel_ptr(), dim3(np * (unsigned)bg_endkey_blocks()), dim3(256), xargs, 0, fs));
+        F.keys = S.keys.as<unsigned long long>();
         F.phase = BG_PH_HEAD;
         BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
         if (h->splitItems > 0)

@@ -455,6 +455,42 @@ __global__ __launch_bounds__(R >= 8 ? 512 : 1024) void bg_exit_conc_kernel(BgSpl
   }
 }
 
+// End-cell keys of the split pairs (few long pairs: one traceback workgroup scanning a 100 k row
+// and column took 0.2 ms): kEndKeyBlocks workgroups per pair fold strided slices of row n1 (the
+// last strip's boundary row, M = M' + a(n1 + j)) and column n2 (M(i, n2)) into the two u64 maxima
+// bg_finish_kernel's HEAD phase then reads (i, j >= 1; it adds the border cells itself).
+constexpr int kEndKeyBlocks = 64;
+__global__ __launch_bounds__(256) void bg_endkey_kernel(BgSplitArgs A) {
+  const int p = (int)blockIdx.x / kEndKeyBlocks, part = (int)blockIdx.x % kEndKeyBlocks;
+  const BgPair P = A.pairs[p];
+  const int n1 = P.n1, n2 = P.n2;
+  if (P.nstrips == 0 || n1 <= 0 || n2 <= 0) return;
+  const int a = A.open;
+  const int stride = kEndKeyBlocks * 256;
+  const int t = part * 256 + (int)threadIdx.x;
+  const int32_t* row = A.bndM + P.bnd_off + (size_t)(P.nstrips - 1) * P.nc * 64;
+  const int32_t* col = A.aux + P.aux_off;
+  u64 kr = 0, kc = 0;
+#pragma unroll 8
+  for (int j = 1 + t; j <= n2; j += stride) {
+    const u64 key = ((u64)key_bias(wadd(row[j], wmul(a, n1 + j))) << 32) | (unsigned)j;
+    kr = key > kr ? key : kr;
+  }
+#pragma unroll 8
+  for (int i = 1 + t; i <= n1; i += stride) {
+    const u64 key = ((u64)key_bias(col[i]) << 32) | (0xFFFFFFFFu - (unsigned)i);
+    kc = key > kc ? key : kc;
+  }
+  kr = wave_umax64(kr);
+  kc = wave_umax64(kc);
+  if ((threadIdx.x & 63) == 0) {
+    if (kc) __hip_atomic_fetch_max(A.endKeys + 2 * (size_t)p, kc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kr) __hip_atomic_fetch_max(A.endKeys + 2 * (size_t)p + 1, kr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+extern "C" void* bg_endkey_kernel_ptr(void) { return (void*)&bg_endkey_kernel; }
+extern "C" int bg_endkey_blocks(void) { return kEndKeyBlocks; }
+
 // One workgroup per (pair, strip s in [1, start strip]): resolves the strip's frontiers segment
 // by segment (segment g's symbols refer to segment g - 1's last frontier), then the bottom row.
 template <int R>
