@@ -123,6 +123,8 @@ struct BgSplitArgs {
   // traceback's HEAD phase: [2p] column n2 (bias(M) << 32 | ~i), [2p + 1] row n1 (| j)
   unsigned long long* endKeys;
   const int32_t* aux;      // the slot's aux arena (column n2: M(i, n2) at aux_off + i)
+  int2* xcount;            // deferred expansion: per (pair, block) ops consuming s1 / s2
+  int32_t xblocks;         // deferred expansion: blocks per pair
 };
 
 // Would the reference SequenceAligner, whose scratch is rows x cols when this call starts
@@ -264,7 +266,9 @@ enum {
   BG_FIN_SYNC = 8,         // linear checkpoint traceback: recompute at barriers (BG_FIN_SYNC=1, A/B)
   BG_FIN_SELFSERVE = 16,   // asynchronous traceback: the walker recomputes every miss itself at
                            // once (tests the forward-progress path; BG_FIN_SELFSERVE=1)
-  BG_FIN_NOPRIO = 32       // the walker keeps priority 0 (A/B of its s_setprio 3; BG_FIN_NOPRIO=1)
+  BG_FIN_NOPRIO = 32,      // the walker keeps priority 0 (A/B of its s_setprio 3; BG_FIN_NOPRIO=1)
+  BG_FIN_DEFER_EXPAND = 64 // split TAIL: the core's op packing and expansion are left to
+                           // bg_expand_count_kernel / bg_expand_kernel (many workgroups per pair)
 };
 
 // bg_pair_result of include/biogarden_gpu.h, as the export kernel writes it.

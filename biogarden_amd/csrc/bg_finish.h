@@ -1316,7 +1316,9 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   gap_run(base, colcase ? f.s1 : f.s2, npre);
   gap_run(cap - ntail, colcase ? f.s1 + ei : f.s2 + ej, ntail);
 
-  // ---------------- expand the walk's op codes into both strings (parallel scan over columns)
+  // ---------------- expand the walk's op codes into both strings (parallel scan over columns);
+  // a split pair's TAIL leaves this to the many-workgroup expansion (BG_FIN_DEFER_EXPAND)
+  if (!(ph == BG_PH_TAIL && (F.flags & BG_FIN_DEFER_EXPAND))) {
   const int i0 = kstop, j0 = lstop;                    // first residues the core consumes
   const int cbase = base + npre;
   const int seg = (ncore + NT - 1) / NT;
@@ -1402,6 +1404,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         ob[x0 + u] = c1v[u];
         ob2[x0 + u] = (F.flags & BG_FIN_LCS) ? (uint8_t)opv[u] : c2v[u];   // LCS: the caller keeps op-0 columns
       }
+  }
   }
   if (tid == 0) {
     BgResult res;

@@ -34,6 +34,8 @@ extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt);
 extern "C" void* bg_finish_ck_kernel_ptr(int R, int mode);
 extern "C" void* bg_split_kernel_ptr(int R, int which);
 extern "C" void* bg_endkey_kernel_ptr(void);
+extern "C" void* bg_expand_kernel_ptr(int which);
+extern "C" int bg_expand_cols_per_block(void);
 extern "C" int bg_endkey_blocks(void);
 extern "C" int bg_exit_lds_bytes(int R);
 extern "C" int bg_exit_conc_lds_bytes(int R);
@@ -137,6 +139,7 @@ struct PhaseTimer {
 struct Slot {
   DevBuf trace, bndM, bndX, aux, out1, out2, results, ops, gran, split, gprog;
   DevBuf keys;                      // split pairs: bg_endkey_kernel's end-cell keys (2 u64 per pair)
+  DevBuf xcnt;                      // split pairs: the deferred expansion's per-block counts
   hipEvent_t dpDone = nullptr, finDone = nullptr;
   hipEvent_t resetDone = nullptr;   // the DP's progress words zeroed (the concurrent exit pass waits)
   bool inflight = false;
@@ -204,6 +207,7 @@ struct bg_aligner {
   std::vector<int2> splitMap;
   std::vector<int32_t> splitBases;  // exit-pass item bases (np + 1), then resolve bases (np + 1),
                                     // then the items in estimated readiness order (concurrent pass)
+  int splitXBlocks = 1;             // deferred expansion: blocks per split pair (max n1 + n2 / 4096)
   int splitConc = 0;                // the exit pass beside the DP: 1 always (BG_SPLIT_CONC=1), 0 never
                                     // (=0), 2 (unset) when no other execute's DP is in flight
   DevBuf splitMapBuf, splitBaseBuf;
@@ -331,7 +335,7 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
   for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
   for (Slot& S : h->slot) {
     for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops, &S.gran, &S.split,
-                      &S.gprog, &S.keys})
+                      &S.gprog, &S.keys, &S.xcnt})
       d->release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
     if (S.finDone) (void)hipEventDestroy(S.finDone);
@@ -1000,6 +1004,12 @@ plan_again:
         for (int s2 = 0; s2 < P.nstrips; ++s2) h->splitMap.push_back(make_int2((int)q, s2));
       }
       h->splitItems = h->splitBases[np];
+      {
+        long capMax = 1;
+        for (const BgPair& P : h->plan) capMax = std::max(capMax, (long)P.n1 + P.n2);
+        const long cols = bg_expand_cols_per_block();
+        h->splitXBlocks = (int)((capMax + cols - 1) / cols);
+      }
       h->splitResolve = h->splitBases[2 * np + 1];
       // the concurrent pass takes items in the order the DP makes them ready: strip s reaches
       // chunk c at about (3 s + c) chunk times (a strip starts ~3 chunks after the one above)
@@ -1046,6 +1056,7 @@ plan_again:
         !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) || !S.ops.ensure(po + 16) ||
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)) ||
         (h->split && !S.keys.ensure(16 * (h->plan.size() + 1))) ||
+        (h->split && !S.xcnt.ensure(8 * ((size_t)h->plan.size() * h->splitXBlocks + 1))) ||
         (h->split && S.split.cap < h->splitInts * 4 + 256 &&
          (!S.split.ensure(h->splitInts * 4 + 256) || hipMemset(S.split.p, 0, S.split.cap) != hipSuccess)) ||
         (h->wide && !S.gprog.ensure(4 * ((size_t)h->progWords + 8))))
@@ -1341,6 +1352,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     X.dpWgs = h->gridWgs;
     X.endKeys = S.keys.as<unsigned long long>();
     X.aux = S.aux.as<int32_t>();
+    X.xcount = S.xcnt.as<int2>();
+    X.xblocks = h->splitXBlocks;
     X.diag = S.gprog.as<uint32_t>() + h->progWords + 2;
     {
       const char* ew = std::getenv("BG_SPLIT_WAIT_MS");
@@ -1450,7 +1463,17 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
         F.phase = BG_PH_WALK;
         BG_HIP(hipLaunchKernel(ffn, dim3((unsigned)h->splitMap.size()), dim3(64 * fnw), args, lds, fs));
         F.phase = BG_PH_TAIL;
+        // the core's packing and expansion by many workgroups per pair (bg_split.hip)
+        const bool defer = !std::getenv("BG_NO_DEFER_EXPAND");
+        if (defer) F.flags |= BG_FIN_DEFER_EXPAND;
         BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
+        if (defer) {
+          F.flags &= ~BG_FIN_DEFER_EXPAND;
+          void* eargs[] = {&F, &X};
+          const unsigned nb = (unsigned)X.xblocks;
+          BG_HIP(hipLaunchKernel(bg_expand_kernel_ptr(0), dim3(np * nb), dim3(256), eargs, 0, fs));
+          BG_HIP(hipLaunchKernel(bg_expand_kernel_ptr(1), dim3(np * nb), dim3(256), eargs, 0, fs));
+        }
       }
     } else {
       F.win_bytes = bg_finish_window_bytes(h->R, h->affine, np, h->cus);
