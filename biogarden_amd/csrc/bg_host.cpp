@@ -1458,7 +1458,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
           BG_HIP(hipLaunchKernel(bg_split_kernel_ptr(h->R, 0), dim3((h->splitItems + 3) / 4), dim3(256), xargs,
                                  bg_exit_lds_bytes(h->R), fs));
         if (h->splitResolve > 0)
-          BG_HIP(hipLaunchKernel(bg_split_kernel_ptr(h->R, 1), dim3(h->splitResolve), dim3(256), xargs, 0, fs));
+          BG_HIP(hipLaunchKernel(bg_split_kernel_ptr(h->R, 1), dim3(h->splitResolve), dim3(64), xargs, 0, fs));
         BG_HIP(hipLaunchKernel(bg_split_kernel_ptr(h->R, 2), dim3(np), dim3(64), xargs, 0, fs));
         F.phase = BG_PH_WALK;
         BG_HIP(hipLaunchKernel(ffn, dim3((unsigned)h->splitMap.size()), dim3(64 * fnw), args, lds, fs));

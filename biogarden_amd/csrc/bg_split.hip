@@ -586,7 +586,9 @@ extern "C" void* bg_expand_kernel_ptr(int which) {
 extern "C" int bg_expand_cols_per_block(void) { return kXCols; }
 
 // One workgroup per (pair, strip s in [1, start strip]): resolves the strip's frontiers segment
-// by segment (segment g's symbols refer to segment g - 1's last frontier), then the bottom row.
+// by segment (segment g's symbols refer to segment g - 1's last frontier).  The bottom row's
+// symbolic exits are resolved by the chain, for the one column per strip it reads (resolving
+// all n2 + 1 of every strip here took 0.2 ms for C3).
 template <int R>
 __global__ __launch_bounds__(256) void bg_exit_resolve_kernel(BgSplitArgs A) {
   constexpr int F = (R + 1) * 64;
@@ -605,69 +607,42 @@ __global__ __launch_bounds__(256) void bg_exit_resolve_kernel(BgSplitArgs A) {
   const int tid = threadIdx.x;
   const int32_t* fr = ar + L.front + (size_t)s * L.G * F;
   int32_t* fs = ar + L.fres + (size_t)s * L.G * F;
-  int* prev = fa;
-  int* cur = fb;
-  for (int x = tid; x < F; x += blockDim.x) { prev[x] = fr[x]; fs[x] = fr[x]; }
-  // The segments form a chain (segment g's symbols point into g - 1's resolved frontier), but
-  // their raw frontiers do not depend on it: each thread keeps the raw values of the next D
-  // segments in flight, so a link costs an LDS lookup and a barrier, not an HBM round trip.
-  // (The 256 threads cover F <= 704 entries in QF passes.)
-  constexpr int D = 8, QF = (F + 255) / 256;
-  int raw[D][QF];
-  auto fetch = [&](int g, int (&r)[QF]) {
+  // The segments form a chain (segment g's symbols point into g - 1's resolved frontier), walked
+  // by wave 0 alone: a wave's LDS operations complete in order, so a link costs its lookups, not
+  // a workgroup barrier.  The raw frontiers do not depend on the chain: each lane keeps the raw
+  // values of the next D segments in flight, so a link is not an HBM round trip either.
+  if (tid < 64) {
+    int* prev = fa;
+    int* cur = fb;
+    constexpr int D = 8, QW = (F + 63) / 64;
+    for (int x = tid; x < F; x += 64) { prev[x] = fr[x]; fs[x] = fr[x]; }
+    int raw[D][QW];
+    auto fetch = [&](int g, int (&r)[QW]) {
 #pragma unroll
-    for (int q = 0; q < QF; ++q) {
-      const int x = tid + 256 * q;
-      r[q] = (g + 1 < L.G && x < F) ? fr[(size_t)g * F + x] : 0;
-    }
-  };
+      for (int q = 0; q < QW; ++q) {
+        const int x = tid + 64 * q;
+        r[q] = (g + 1 < L.G && x < F) ? fr[(size_t)g * F + x] : 0;
+      }
+    };
 #pragma unroll
-  for (int d = 0; d < D; ++d) fetch(1 + d, raw[d]);
-  __syncthreads();
-  for (int g0 = 1; g0 + 1 < L.G; g0 += D) {
+    for (int d = 0; d < D; ++d) fetch(1 + d, raw[d]);
+    for (int g0 = 1; g0 + 1 < L.G; g0 += D) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const int g = g0 + d;
-      if (g + 1 >= L.G) break;                           // block-uniform
+      for (int d = 0; d < D; ++d) {
+        const int g = g0 + d;
+        if (g + 1 >= L.G) break;                         // wave-uniform
 #pragma unroll
-      for (int q = 0; q < QF; ++q) {
-        const int x = tid + 256 * q;
-        if (x < F) {
-          const int rv = raw[d][q];
-          const int v = rv >= kSym ? prev[rv - kSym] : rv;
-          cur[x] = v;
-          fs[(size_t)g * F + x] = v;
+        for (int q = 0; q < QW; ++q) {
+          const int x = tid + 64 * q;
+          if (x < F) {
+            const int rv = raw[d][q];
+            const int v = rv >= kSym ? prev[rv - kSym] : rv;
+            cur[x] = v;
+            fs[(size_t)g * F + x] = v;
+          }
         }
-      }
-      fetch(g + D, raw[d]);                              // this slot's next segment
-      __syncthreads();
-      int* t = prev; prev = cur; cur = t;
-    }
-  }
-  __threadfence_block();
-  __syncthreads();
-  if (s < sStar) {
-    // rounds of EBK columns: the raw exits, then the lookups they need, then the stores (a load
-    // after a store to a possibly aliasing buffer would wait a round trip per column)
-    constexpr int EBK = 8;
-    int32_t* eb = ar + L.ebot + (size_t)s * (n2 + 1);
-    for (int j0 = tid; j0 <= n2; j0 += EBK * 256) {
-      int rv[EBK], nv[EBK];
-#pragma unroll
-      for (int u = 0; u < EBK; ++u) {
-        const int j = j0 + 256 * u;
-        rv[u] = j <= n2 ? eb[j] : 0;
-      }
-#pragma unroll
-      for (int u = 0; u < EBK; ++u) {
-        const int j = j0 + 256 * u;
-        const int seg = ((j + 63) >> 6) / A.segc;       // lane 63 is at column j at step j + 63
-        nv[u] = rv[u] < kSym ? rv[u] : (seg >= 1 ? fs[(size_t)(seg - 1) * F + (rv[u] - kSym)] : -1);
-      }
-#pragma unroll
-      for (int u = 0; u < EBK; ++u) {
-        const int j = j0 + 256 * u;
-        if (j <= n2 && rv[u] >= kSym) eb[j] = nv[u];
+        fetch(g + D, raw[d]);                            // this slot's next segment
+        int* t = prev; prev = cur; cur = t;
       }
     }
   }
@@ -701,7 +676,14 @@ __global__ __launch_bounds__(64) void bg_exit_chain_kernel(BgSplitArgs A) {
           ar[L.startcol + s] = c;
           lo = s;
           if (s == 0) break;
-          c = ar[L.ebot + (size_t)s * (n2 + 1) + c];
+          // strip s's bottom-row exit at column c, resolved here when symbolic (the resolve
+          // kernel only resolves the frontiers: the chain reads one column per strip)
+          int v = ar[L.ebot + (size_t)s * (n2 + 1) + c];
+          if (v >= kSym) {
+            const int seg = ((c + 63) >> 6) / A.segc;     // lane 63 is at column c at step c + 63
+            v = seg >= 1 ? ar[L.fres + ((size_t)s * L.G + seg - 1) * F + (v - kSym)] : -1;
+          }
+          c = v;
         }
       }
     }
