@@ -236,11 +236,17 @@ __device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
     }
     return false;
   };
-  // polls back off (~0.2 us, then ~1.7 us apart): thousands of waiting waves' loads otherwise
+  // polls back off (~0.2 us, then ~1.7 us, then ~7 us apart): thousands of waiting waves' loads otherwise
   // compete with the DP's own hand-offs in L2
   auto backoff = [&]() {
-    if (np < 16) __builtin_amdgcn_s_sleep(8);
-    else __builtin_amdgcn_s_sleep(63);
+    if (np < 16) {
+      __builtin_amdgcn_s_sleep(8);
+    } else if (np < 64) {
+      __builtin_amdgcn_s_sleep(63);
+    } else {                                             // a long wait: ~7 us between polls
+      __builtin_amdgcn_s_sleep(127);
+      __builtin_amdgcn_s_sleep(127);
+    }
   };
   // the top block of chunk c (columns c*64 + lane, clamped to n2)
   auto top_abs = [&](int c) {
