@@ -398,9 +398,14 @@ __device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
       if (capHere) exit_chunk<R, false, true>(S, c, lane, profLane, codeLane, bIn, col0, ts, qs, rs, cap);
       else exit_chunk<R, false, false>(S, c, lane, profLane, codeLane, bIn, col0, ts, qs, rs, cap);
     }
-    if (capHere && lane == 0) {
-      ar[L.head + 4] = (int)(cap & kEMask);
-      ar[L.head + 5] = g;
+    if (capHere) {
+      if (lane == 0) {
+        ar[L.head + 4] = (int)(cap & kEMask);
+        ar[L.head + 5] = g;
+      }
+      // the start strip's later chunks feed nothing: its bottom row is not needed (the walk
+      // starts inside it) and the chain resolves the capture through the frontier before it
+      if (capItem) return;
     }
     // the bottom row (lane 63's last row) of steps t0 .. t0 + 63: columns t0 - 63 + lane
     if (wantBot) {
