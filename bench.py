@@ -46,15 +46,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (default 4) round-robin;
-# with fewer queues than the host_to_host leg's streams, a handle's string download waits in a
-# queue behind another handle's DP kernel (fetch D2H 1.7-2.1 ms per batch against 0.41 ms with a
-# queue per stream; profiles/r03/h2h_queues/).  Read by HIP at its initialisation: a value the
-# environment sets is kept (and the leg sizes its handle rotation to it, host_to_host.hw_queues);
-# only when unset does the bench ask for 16.
+# HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default, and what the
+# MI355X boxes' environment sets).  The bench never raises it: the streaming leg (host_to_host)
+# shares one set of four streams between its handles, so it fits four queues.
 HW_QUEUES_ENV = os.environ.get("GPU_MAX_HW_QUEUES")
-if not HW_QUEUES_ENV:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 from tools import workloads  # noqa: E402
 
@@ -254,16 +249,19 @@ def sharded_job(pairs, mode, a, b, world, rank):
     return [pairs[p] for p in mine], shard.shard_call_dims(mode, sizes, a, b, mine), shards
 
 
-def host_to_host(pairs, mode, a, b, device, rounds=8, pipeline=3, handles=4):
+def host_to_host(pairs, mode, a, b, device, rounds=8, pipeline=2, handles=4, shared=True):
     """PCIe-inclusive throughput through the product's streaming API (biogarden_amd.stream.
     AlignStream): per batch the residues are staged from host buffers (validation, pinned
     staging, H2D), the kernels run, and the aligned strings come back into host buffers; the
     stream's handle rotation keeps `handles` batches in flight so uploads, downloads and the
-    host's byte passes overlap the kernels."""
+    host's byte passes overlap the kernels.  The handles share one set of four HIP streams
+    (uploads, DPs, tracebacks, downloads), so the leg fits the box's 4 hardware queues.  This is
+    SURVEY §8(d)'s wall: H2D of the residues, DP, end cell, traceback and the strings on the
+    host."""
     from biogarden_amd.alignment import score
     from biogarden_amd.stream import AlignStream
     with AlignStream(mode, score.blosum62, a, b, device=device, handles=handles,
-                     pipeline=pipeline, raw=True) as st:
+                     pipeline=pipeline, raw=True, shared=shared) as st:
         for _ in range(handles):                       # warm every handle's arenas
             st.submit(pairs)
         st.drain()
@@ -286,9 +284,13 @@ def host_to_host(pairs, mode, a, b, device, rounds=8, pipeline=3, handles=4):
             "seconds_per_batch": round(secs / rounds, 5),
             "host_ms_per_batch": phases, "host_threads": int(ht.get("host_threads", 0)),
             "prepares": int(ht.get("prepares", 0)), "fetches": int(ht.get("fetches", 0)),
+            "streams": 4 if shared else 3 * handles, "shared_streams": shared,
             "covers": "biogarden_amd.stream.AlignStream: bg_batch_prepare (validation, pinned "
-                      "staging, H2D) + execute + bg_batch_fetch (D2H, aligned strings in host "
-                      "buffers), %d handles in rotation" % handles}
+                      "staging, H2D) + execute + the strings' D2H queued behind the traceback + "
+                      "bg_batch_fetch (aligned strings in host buffers), %d handles in rotation "
+                      "on %s" % (handles, "one shared set of 4 HIP streams" if shared
+                                 else "streams of their own"),
+            "survey_8d_wall": True}
 
 
 def cpu_section(pairs, gpu_scores, mode, a, b, info, pairs_multi, pairs_one):
@@ -428,9 +430,10 @@ def main():
     ap.add_argument("--no-affine", action="store_true")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host timing")
-    ap.add_argument("--h2h-handles", type=int, default=0,
-                    help="handles in the host-to-host rotation (0: 4 when the process has >= 12 "
-                         "hardware queues, else 2)")
+    ap.add_argument("--h2h-handles", type=int, default=4,
+                    help="handles (batches in flight) in the host-to-host rotation")
+    ap.add_argument("--h2h-unshared", action="store_true",
+                    help="host-to-host handles on streams of their own (round-4 layout, A/B)")
     ap.add_argument("--h2h-rounds", type=int, default=24,
                     help="timed batches of the host-to-host leg (the stream's fill and drain, "
                          "~one batch's latency, spread over them)")
@@ -571,11 +574,11 @@ def main():
     h2h = None
     if not args.no_h2h:
         queues = int(os.environ.get("GPU_MAX_HW_QUEUES") or 4)
-        nh = args.h2h_handles or (4 if queues >= 12 else 2)
         h2h = host_to_host(pairs, args.mode, args.open, args.extend, local_rank,
-                           pipeline=args.pipeline, handles=nh, rounds=args.h2h_rounds)
+                           handles=args.h2h_handles, rounds=args.h2h_rounds,
+                           shared=not args.h2h_unshared)
         h2h["hw_queues"] = queues
-        h2h["hw_queues_source"] = "environment" if HW_QUEUES_ENV else "bench default (unset)"
+        h2h["hw_queues_source"] = "environment" if HW_QUEUES_ENV else "HIP default (unset)"
 
     if rank != 0:
         h.close()
@@ -621,6 +624,9 @@ def main():
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         "gather_record_bytes_per_rank": gstats.get("record_bytes"),
         "host_to_host": h2h,
+        # SURVEY §8(d) defines GCUPS over a wall that includes H2D, traceback and the strings on
+        # the host: that is host_to_host (value is the build contract's HBM-resident rate)
+        "survey_8d_wall_gcups": None if h2h is None else h2h["gcups"],
         "all_status_ok": ok_status,
     }
     print(json.dumps(line))

@@ -25,7 +25,10 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_aligner_set_call_dims", "bg_host_timing", "bg_last_hip_error",
            "bg_batch_export_compact", "bg_compact_expand", "bg_fasta_open",
            "bg_batch_prepare_table", "bg_fasta_next_batch",
-           "bg_fasta_close", "bg_split_stats", "bg_split_conc_diag"]
+           "bg_fasta_close", "bg_split_stats", "bg_split_conc_diag", "bg_aligner_new_shared",
+           "bg_set_async_fetch", "bg_group_new", "bg_group_free", "bg_group_size",
+           "bg_group_member", "bg_group_align_batch", "bg_group_plan", "bg_group_buffer_size",
+           "bg_group_timing"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -93,6 +96,9 @@ def lib():
     L.bg_scoring_builtin.argtypes = [ctypes.c_int, ctypes.POINTER(BgScoring)]
     L.bg_aligner_new.argtypes = [ctypes.c_int]
     L.bg_aligner_new.restype = ctypes.c_void_p
+    L.bg_aligner_new_shared.argtypes = [ctypes.c_void_p]
+    L.bg_aligner_new_shared.restype = ctypes.c_void_p
+    L.bg_set_async_fetch.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.bg_aligner_free.argtypes = [ctypes.c_void_p]
     L.bg_aligner_free.restype = None
     L.bg_align.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t,
@@ -148,6 +154,22 @@ def lib():
     L.bg_edit_distance_batch.argtypes = pair_args + [ctypes.POINTER(ctypes.c_uint64)]
     L.bg_lcs_batch.argtypes = pair_args + [c_u8p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64),
                                            ctypes.POINTER(ctypes.c_uint64)]
+    L.bg_group_new.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    L.bg_group_new.restype = ctypes.c_void_p
+    L.bg_group_free.argtypes = [ctypes.c_void_p]
+    L.bg_group_free.restype = None
+    L.bg_group_size.argtypes = [ctypes.c_void_p]
+    L.bg_group_member.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.bg_group_member.restype = ctypes.c_void_p
+    L.bg_group_align_batch.argtypes = [ctypes.c_void_p] + batch_args[1:] + [
+        ctypes.POINTER(BgPairResult), c_u8p, c_u8p, ctypes.c_size_t]
+    L.bg_group_plan.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+                                ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_int32)]
+    L.bg_group_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                                       ctypes.POINTER(ctypes.c_size_t)]
+    L.bg_group_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.c_size_t,
+                                  ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.bg_fasta_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]
     L.bg_fasta_open.restype = ctypes.c_void_p
     L.bg_fasta_next_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
@@ -177,10 +199,15 @@ def check(rc):
 
 
 class Handle:
-    """One bg_aligner (device scratch arenas + HIP stream) on one GPU."""
+    """One bg_aligner (device scratch arenas + HIP streams) on one GPU.  share=<Handle>: a handle
+    on the same GPU that shares that handle's HIP streams (bg_aligner_new_shared)."""
 
-    def __init__(self, device=0):
-        self._p = lib().bg_aligner_new(int(device))
+    def __init__(self, device=0, share=None):
+        if share is not None:
+            self._p = lib().bg_aligner_new_shared(share._p)
+            device = share.device
+        else:
+            self._p = lib().bg_aligner_new(int(device))
         if not self._p:
             raise NativeUnavailable("bg_aligner_new(%d) failed: no usable HIP device" % device)
         self.device = device
@@ -206,6 +233,11 @@ class Handle:
 
     def set_pipeline(self, depth):
         check(lib().bg_set_pipeline(self._p, depth))
+
+    def set_async_fetch(self, on=True):
+        """bg_set_async_fetch: every execute queues its results' download behind its traceback;
+        fetch() then only waits and unpacks."""
+        check(lib().bg_set_async_fetch(self._p, 1 if on else 0))
 
     @staticmethod
     def _arrays(pairs):
@@ -412,6 +444,79 @@ class Handle:
         v = (ctypes.c_uint32 * 6)()
         check(lib().bg_split_conc_diag(self._p, v))
         return dict(zip(("abandoned", "item", "input", "tag_seen", "epoch", "not_resident"), list(v)))
+
+
+class Group:
+    """bg_group: one process driving several GPUs (a device may repeat: several shards on one
+    GPU).  align_batch splits the pairs over the members by cells, aligns every shard on its
+    device, gathers the compact records to the first member's device over RCCL and expands them
+    on the host — the same results as Handle.align_batch on one aligner."""
+
+    PHASES = ("prepare_execute", "export", "gather", "download", "expand")
+
+    def __init__(self, devices):
+        devs = (ctypes.c_int * len(devices))(*devices)
+        self._p = lib().bg_group_new(devs, len(devices))
+        if not self._p:
+            raise NativeUnavailable("bg_group_new(%r) failed (no such device, or no librccl)"
+                                    % (list(devices),))
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "_p", None):
+            lib().bg_group_free(self._p)
+            self._p = None
+
+    __del__ = close
+
+    def __len__(self):
+        return lib().bg_group_size(self._p)
+
+    def align_batch_raw(self, mode, pairs, scoring, a, b):
+        """-> (results ctypes array, out1, out2) without per-pair Python objects."""
+        a1, n1, a2, n2, total = Handle._arrays(pairs)
+        n = len(pairs)
+        res = (BgPairResult * max(n, 1))()
+        o1 = (ctypes.c_uint8 * max(total, 1))()
+        o2 = (ctypes.c_uint8 * max(total, 1))()
+        check(lib().bg_group_align_batch(self._p, MODES.get(mode, mode), n, a1, n1, a2, n2,
+                                         ctypes.byref(scoring), a, b, res, o1, o2, total))
+        return res, o1, o2
+
+    def align_batch(self, mode, pairs, scoring, a, b):
+        res, o1, o2 = self.align_batch_raw(mode, pairs, scoring, a, b)
+        b1, b2 = bytes(o1), bytes(o2)
+        out = []
+        for p in range(len(pairs)):
+            r = res[p]
+            lo, hi = r.offset, r.offset + r.len
+            out.append({"status": r.status, "score": r.score, "aligned1": b1[lo:hi],
+                        "aligned2": b2[lo:hi], "end": (r.end_i, r.end_j),
+                        "start": (r.start1, r.start2)})
+        return out
+
+    def buffer_size(self):
+        r, c = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib().bg_group_buffer_size(self._p, ctypes.byref(r), ctypes.byref(c)))
+        return r.value, c.value
+
+    def timing(self, reset=False):
+        ms = (ctypes.c_double * 5)()
+        calls = ctypes.c_uint64()
+        check(lib().bg_group_timing(self._p, ms, 5, ctypes.byref(calls), 1 if reset else 0))
+        out = {k: ms[i] for i, k in enumerate(self.PHASES)}
+        out["calls"] = calls.value
+        return out
+
+
+def group_plan(sizes, nshards):
+    """bg_group_plan (host only): the member of every pair, [(n1, n2)] -> [int]."""
+    n = len(sizes)
+    n1 = (ctypes.c_size_t * max(n, 1))(*[x for x, _ in sizes])
+    n2 = (ctypes.c_size_t * max(n, 1))(*[y for _, y in sizes])
+    out = (ctypes.c_int32 * max(n, 1))()
+    check(lib().bg_group_plan(n, n1, n2, nshards, out))
+    return [out[p] for p in range(n)]
 
 
 def expand_compact(rec, pairs):

@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <thread>
@@ -145,10 +146,30 @@ struct Slot {
   bool inflight = false;
 };
 
+// The HIP streams of one handle, or of several handles on one device that share them
+// (bg_aligner_new_shared).  HIP maps a process's streams onto GPU_MAX_HW_QUEUES hardware queues
+// (4 on the MI355X boxes); a stream sharing a queue with another stream's kernels waits behind
+// them.  Handles in rotation (biogarden_amd/stream.py) therefore share ONE set: uploads, DPs,
+// tracebacks and downloads each get their own stream and queue however many batches are in
+// flight, and the DPs / tracebacks of consecutive batches pipeline exactly as the executes of one
+// handle do.  Streams beyond the first two are created on first use.
+enum { kSDp, kSFin, kSFin2, kSFin3, kSDps, kSUp, kSDl, kSN };
+struct StreamGroup {
+  int device = 0;
+  hipStream_t s[kSN] = {};
+  std::mutex mu;
+  ~StreamGroup() {
+    (void)hipSetDevice(device);
+    for (hipStream_t x : s)
+      if (x) { (void)hipStreamSynchronize(x); (void)hipStreamDestroy(x); }
+  }
+};
+
 struct bg_aligner {
   int device = 0;
   int cus = 256;
-  hipStream_t stream = nullptr;    // uploads, DP kernels, downloads
+  std::shared_ptr<StreamGroup> sg; // the stream set (shared with other handles, or this one's)
+  hipStream_t stream = nullptr;    // DP kernels (and, unshared, uploads and downloads)
   hipStream_t stream2 = nullptr;   // end cell + traceback kernels
   hipStream_t stream3 = nullptr;   // WIDE batches: every other execute's traceback (see execute)
   hipStream_t stream4 = nullptr;   // WIDE batches at pipeline depth 4: every third one
@@ -156,6 +177,19 @@ struct bg_aligner {
   // 256), so two executes' DPs run side by side on disjoint CUs (each waits for its own slot's
   // previous traceback); created on first use (BG_TWO_DP_STREAMS=1)
   hipStream_t dps = nullptr;
+  hipStream_t upS = nullptr;       // shared handles: uploads (a queue of their own)
+  hipStream_t dlS = nullptr;       // downloads of the asynchronous fetch (bg_set_async_fetch)
+  // bg_set_async_fetch: every execute queues its results' download (into ho1 / ho2 / hresPin)
+  // right after its traceback; bg_batch_fetch then only waits for it and unpacks
+  int asyncFetch = 0;
+  int dlExec = -1;                 // the execute (execCount) whose download was queued last
+  hipEvent_t dlDone = nullptr;
+  uint64_t planOut = 0;            // prepared batch: sum of n1 + n2 over the plan's pairs
+  hipEvent_t upDone = nullptr;     // shared handles: the prepared batch's upload (not waited for
+  bool upPending = false;          // on the host; the DPs wait for it)
+  std::vector<int32_t> profHost;   // the prepared batch's profile table and result templates,
+  std::vector<BgPairResultDev> tmplHost;   // kept until the upload has read them
+  bool shared() const { return sg && sg.use_count() > 1; }
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // last execute: dp start/end, fin start/end
   DevBuf seq1, seq2, codes1, codes2, lut, prof, pairs, recs;
   Slot slot[4];
@@ -227,6 +261,7 @@ struct bg_aligner {
 
   std::vector<BgResult> hres;
   PinBuf ho1, ho2;                 // fetch: the slot's aligned strings, downloaded
+  PinBuf hresPin;                  // asynchronous fetch: the results, downloaded
   PinBuf up;                       // prepare: raw residues + codes of the batch, uploaded
   std::vector<uint32_t> pmask;     // prepare: per pair, the score codes its residues use
   std::vector<uint64_t> coff1, coff2;   // prepare: caller-order offsets of the staged residues
@@ -295,7 +330,34 @@ extern "C" const char* bg_status_string(int s) {
 
 extern "C" int bg_abi_version(void) { return BG_ABI_VERSION; }
 
-extern "C" bg_aligner* bg_aligner_new(int device) {
+// The group's stream `which`, created on first use (nullptr if HIP cannot create it)
+static hipStream_t group_stream(bg_aligner* h, int which) {
+  StreamGroup& G = *h->sg;
+  std::lock_guard<std::mutex> lk(G.mu);
+  if (!G.s[which] && hipStreamCreateWithFlags(&G.s[which], hipStreamNonBlocking) != hipSuccess)
+    G.s[which] = nullptr;
+  return G.s[which];
+}
+
+// Waits for this handle's own work.  A handle alone on its streams waits for the streams; a handle
+// sharing them waits for its own events only (every execute ends in its slot's finDone, recorded
+// after its DP and traceback; a queued download in dlDone), so other handles' batches keep flowing.
+static hipError_t drain(bg_aligner* h) {
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return e;
+  if (!h->shared()) {
+    for (hipStream_t s : {h->stream, h->stream2, h->stream3, h->stream4, h->dps, h->upS, h->dlS})
+      if (s && (e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    return hipSuccess;
+  }
+  for (const Slot& S : h->slot)
+    if (S.inflight && (e = hipEventSynchronize(S.finDone)) != hipSuccess) return e;
+  if (h->dlExec >= 0 && (e = hipEventSynchronize(h->dlDone)) != hipSuccess) return e;
+  if (h->upPending && (e = hipEventSynchronize(h->upDone)) != hipSuccess) return e;
+  return hipSuccess;
+}
+
+static bg_aligner* aligner_init(int device, const std::shared_ptr<StreamGroup>& share) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return nullptr;
   if (hipSetDevice(device) != hipSuccess) return nullptr;
@@ -304,14 +366,25 @@ extern "C" bg_aligner* bg_aligner_new(int device) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     h->cus = prop.multiProcessorCount;
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess) {
+  if (share) {
+    h->sg = share;
+  } else {
+    h->sg = std::make_shared<StreamGroup>();
+    h->sg->device = device;
+  }
+  h->stream = group_stream(h, kSDp);
+  h->stream2 = group_stream(h, kSFin);
+  if (!h->stream || !h->stream2) {
     bg_aligner_free(h);
     return nullptr;
   }
   for (auto& e : h->ev)
     if (hipEventCreate(&e) != hipSuccess) { bg_aligner_free(h); return nullptr; }
+  if (hipEventCreateWithFlags(&h->dlDone, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->upDone, hipEventDisableTiming) != hipSuccess) {
+    bg_aligner_free(h);
+    return nullptr;
+  }
   for (Slot& S : h->slot)
     if (hipEventCreateWithFlags(&S.dpDone, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&S.finDone, hipEventDisableTiming) != hipSuccess) {
@@ -321,18 +394,21 @@ extern "C" bg_aligner* bg_aligner_new(int device) {
   return h;
 }
 
+extern "C" bg_aligner* bg_aligner_new(int device) { return aligner_init(device, nullptr); }
+
+extern "C" bg_aligner* bg_aligner_new_shared(bg_aligner* peer) {
+  if (!peer || !peer->sg) return nullptr;
+  return aligner_init(peer->device, peer->sg);
+}
+
 extern "C" void bg_aligner_free(bg_aligner* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
-  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
-  if (h->stream3) (void)hipStreamSynchronize(h->stream3);
-  if (h->stream4) (void)hipStreamSynchronize(h->stream4);
-  if (h->dps) (void)hipStreamSynchronize(h->dps);
+  if (h->sg) (void)drain(h);
   for (DevBuf* d : {&h->seq1, &h->seq2, &h->codes1, &h->codes2, &h->lut, &h->prof, &h->pairs, &h->recs,
                     &h->wgmapBuf, &h->gprogBuf, &h->dbgBuf, &h->dpDbg, &h->profScratch, &h->compactSizes})
     d->release();
-  for (PinBuf* q : {&h->ho1, &h->ho2, &h->up}) q->release();
+  for (PinBuf* q : {&h->ho1, &h->ho2, &h->up, &h->hresPin}) q->release();
   for (Slot& S : h->slot) {
     for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops, &S.gran, &S.split,
                       &S.gprog, &S.keys, &S.xcnt})
@@ -345,11 +421,9 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : h->ring)
     if (e) (void)hipEventDestroy(e);
-  if (h->stream) (void)hipStreamDestroy(h->stream);
-  if (h->stream2) (void)hipStreamDestroy(h->stream2);
-  if (h->stream3) (void)hipStreamDestroy(h->stream3);
-  if (h->stream4) (void)hipStreamDestroy(h->stream4);
-  if (h->dps) (void)hipStreamDestroy(h->dps);
+  if (h->dlDone) (void)hipEventDestroy(h->dlDone);
+  if (h->upDone) (void)hipEventDestroy(h->upDone);
+  h->sg.reset();                   // the last handle of a group destroys its streams
   delete h;
 }
 
@@ -373,11 +447,7 @@ extern "C" int bg_set_kernel_options(bg_aligner* h, int allow_tagged) {
 
 extern "C" int bg_set_pipeline(bg_aligner* h, int depth) {
   if (!h || depth < 1 || depth > 4) return BG_E_ARG;
-  if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
-      hipStreamSynchronize(h->stream2) != hipSuccess || hipStreamSynchronize(h->stream3) != hipSuccess ||
-      (h->stream4 && hipStreamSynchronize(h->stream4) != hipSuccess) ||
-      (h->dps && hipStreamSynchronize(h->dps) != hipSuccess))
-    return BG_E_HIP;
+  if (drain(h) != hipSuccess) return BG_E_HIP;
   h->depth = depth;
   h->prepared = false;   // arenas are sized at prepare time
   h->executed = false;
@@ -402,6 +472,14 @@ static void note_hip(hipError_t e, const char* what, int line) {
   } while (0)
 
 extern "C" int bg_last_hip_error(void) { return g_lastHip; }
+
+extern "C" int bg_set_async_fetch(bg_aligner* h, int on) {
+  if (!h) return BG_E_ARG;
+  BG_HIP(drain(h));
+  h->asyncFetch = on ? 1 : 0;
+  h->dlExec = -1;
+  return BG_OK;
+}
 
 // Strip pipeline of one pair on `gw` waves: phases (64-step chunks) until its last strip ends.
 static int pipeline_phases(int S, int gw, int NC, int lag = 2) {
@@ -708,14 +786,10 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   if (!h->finFlags) callDims = h->callDims;
   PhaseTimer tm(h->hostMs);
   ++h->nPrepare;
-  BG_HIP(hipSetDevice(h->device));
-  BG_HIP(hipStreamSynchronize(h->stream));
-  BG_HIP(hipStreamSynchronize(h->stream2));
-  BG_HIP(hipStreamSynchronize(h->stream3));
-  if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
-  if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
+  BG_HIP(drain(h));
   tm.mark(kPhSync, "sync");
   for (Slot& S : h->slot) S.inflight = false;
+  h->dlExec = -1;
   h->execCount = 0;
   h->prepared = false;
   h->executed = false;
@@ -1057,8 +1131,7 @@ plan_again:
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)) ||
         (h->split && !S.keys.ensure(16 * (h->plan.size() + 1))) ||
         (h->split && !S.xcnt.ensure(8 * ((size_t)h->plan.size() * h->splitXBlocks + 1))) ||
-        (h->split && S.split.cap < h->splitInts * 4 + 256 &&
-         (!S.split.ensure(h->splitInts * 4 + 256) || hipMemset(S.split.p, 0, S.split.cap) != hipSuccess)) ||
+        (h->split && !S.split.ensure(h->splitInts * 4 + 256)) ||
         (h->wide && !S.gprog.ensure(4 * ((size_t)h->progWords + 8))))
       return BG_E_NOMEM;
     // WIDE checkpoint batches hand strip rows between workgroups as epoch-tagged granules: a
@@ -1073,6 +1146,25 @@ plan_again:
   }
 
   tm.mark(kPhAlloc, "alloc");
+  // uploads go on the DP stream of a handle alone, on the group's upload stream otherwise (the DP
+  // stream then holds other handles' DPs, which the upload must not queue behind)
+  hipStream_t us = h->stream;
+  if (h->shared()) {
+    if (!h->upS) h->upS = group_stream(h, kSUp);
+    if (!h->upS) return BG_E_HIP;
+    us = h->upS;
+  }
+  // the split arena holds epoch-tagged words (done tags, checkpoint granules, the head's overflow
+  // tag) beside plain column numbers; a batch with another layout would read the previous batch's
+  // columns where its tags live, and a small column can equal an epoch — zeroed at every prepare
+  if (h->split)
+    for (int z = 0; z < h->depth; ++z)
+      BG_HIP(hipMemsetAsync(h->slot[z].split.p, 0, h->splitInts * 4 + 256, us));
+  // asynchronous fetch: the pinned download buffers sized now, while nothing is in flight
+  h->planOut = oo;
+  if (h->asyncFetch && (!h->ho1.ensure(oo + 1) || !h->ho2.ensure(oo + 1) ||
+                        !h->hresPin.ensure(sizeof(BgResult) * (h->plan.size() + 1))))
+    return BG_E_NOMEM;
   // ---- uploads: the raw residues staged above (one DMA each), the tables; the codes are
   // made on the device (bg_code_kernel)
   uint8_t lut[256];
@@ -1081,7 +1173,9 @@ plan_again:
     const int d = (c < KS && dense[c] >= 0) ? dense[c] : 0;
     lut[x] = (uint8_t)((h->dna && !h->ack) ? d * 8 : d);
   }
-  std::vector<int32_t> prof(std::max<size_t>(1024, (size_t)h->pstride * h->pstride), 0);
+  // (a handle member: a shared handle's upload is still in flight when prepare returns)
+  std::vector<int32_t>& prof = h->profHost;
+  prof.assign(std::max<size_t>(1024, (size_t)h->pstride * h->pstride), 0);
   if (h->ack) {
     int16_t* t16 = reinterpret_cast<int16_t*>(prof.data());
     const int sub = mode == BG_LOCAL ? a : a + b;
@@ -1129,9 +1223,9 @@ plan_again:
   }
   st1[o1] = st2[o2] = 0;
   std::memcpy(st2 + o2 + 16, lut, 256);
-  BG_HIP(hipMemcpyAsync(h->seq1.p, st1, o1 + 1, hipMemcpyHostToDevice, h->stream));
-  BG_HIP(hipMemcpyAsync(h->seq2.p, st2, o2 + 1, hipMemcpyHostToDevice, h->stream));
-  BG_HIP(hipMemcpyAsync(h->lut.p, st2 + o2 + 16, 256, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->seq1.p, st1, o1 + 1, hipMemcpyHostToDevice, us));
+  BG_HIP(hipMemcpyAsync(h->seq2.p, st2, o2 + 1, hipMemcpyHostToDevice, us));
+  BG_HIP(hipMemcpyAsync(h->lut.p, st2 + o2 + 16, 256, hipMemcpyHostToDevice, us));
   {
     const uint8_t* r1 = h->seq1.as<uint8_t>();
     uint8_t* c1 = h->codes1.as<uint8_t>();
@@ -1142,23 +1236,24 @@ plan_again:
     const uint8_t* lt = h->lut.as<uint8_t>();
     void* args[] = {&r1, &c1, &m1, &r2, &c2, &m2, &lt};
     const int blocks = (int)std::min<uint64_t>(4096, std::max<uint64_t>(1, (m1 + m2) / (16 * 256) + 2));
-    BG_HIP(hipLaunchKernel(bg_code_kernel_ptr(), dim3(blocks), dim3(256), args, 0, h->stream));
+    BG_HIP(hipLaunchKernel(bg_code_kernel_ptr(), dim3(blocks), dim3(256), args, 0, us));
   }
-  BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), prof.size() * 4, hipMemcpyHostToDevice, h->stream));
+  BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), prof.size() * 4, hipMemcpyHostToDevice, us));
   if (!h->plan.empty())
     if (h->wide)
     BG_HIP(hipMemcpyAsync(h->wgmapBuf.p, h->wgmap.data(), sizeof(int2) * h->wgmap.size(),
-                          hipMemcpyHostToDevice, h->stream));
+                          hipMemcpyHostToDevice, us));
   BG_HIP(hipMemcpyAsync(h->pairs.p, h->plan.data(), sizeof(BgPair) * h->plan.size(),
-                          hipMemcpyHostToDevice, h->stream));
+                          hipMemcpyHostToDevice, us));
   if (h->split) {
     BG_HIP(hipMemcpyAsync(h->splitMapBuf.p, h->splitMap.data(), sizeof(int2) * h->splitMap.size(),
-                          hipMemcpyHostToDevice, h->stream));
+                          hipMemcpyHostToDevice, us));
     BG_HIP(hipMemcpyAsync(h->splitBaseBuf.p, h->splitBases.data(), 4 * h->splitBases.size(),
-                          hipMemcpyHostToDevice, h->stream));
+                          hipMemcpyHostToDevice, us));
   }
   {
-    std::vector<BgPairResultDev> tmpl(npairs);
+    std::vector<BgPairResultDev>& tmpl = h->tmplHost;
+    tmpl.resize(npairs);
     for (size_t p = 0; p < npairs; ++p) {
       std::memset(&tmpl[p], 0, sizeof(tmpl[p]));
       tmpl[p].status = h->prestatus[p] < 0 ? 0 : h->prestatus[p];
@@ -1167,10 +1262,19 @@ plan_again:
     if (!h->recs.ensure(sizeof(BgPairResultDev) * (npairs + 1))) return BG_E_NOMEM;
     if (npairs)
       BG_HIP(hipMemcpyAsync(h->recs.p, tmpl.data(), sizeof(BgPairResultDev) * npairs,
-                            hipMemcpyHostToDevice, h->stream));
+                            hipMemcpyHostToDevice, us));
   }
   tm.mark(kPhUpload, "queue");
-  BG_HIP(hipStreamSynchronize(h->stream));
+  // a handle alone waits for its upload here; a shared handle does not (the code kernel on the
+  // upload stream needs CUs, which the DP of the batch before holds): its executes' DPs wait for
+  // the upload on the device, and its next prepare drains it (every source stays untouched until
+  // then: the pinned staging and handle-owned vectors)
+  if (h->shared()) {
+    BG_HIP(hipEventRecord(h->upDone, us));
+    h->upPending = true;
+  } else {
+    BG_HIP(hipStreamSynchronize(us));
+  }
   tm.mark(kPhUpload, "upload");
   h->order_ = order;
   h->bufRows = bufR;
@@ -1221,23 +1325,28 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   const char* e2 = std::getenv("BG_TWO_DP_STREAMS");
   if (h->wide && h->depth >= 2 && (h->execCount & 1) && !(e2 && e2[0] == '0') && 2 * h->gridWgs <= h->cus &&
       !std::getenv("BG_DP_TIMING")) {
-    if (!h->dps && hipStreamCreateWithFlags(&h->dps, hipStreamNonBlocking) != hipSuccess) h->dps = nullptr;
+    if (!h->dps) h->dps = group_stream(h, kSDps);
     if (h->dps) ds = h->dps;
   }
   // the exit pass beside the DP needs the CUs this DP leaves idle: in the automatic mode it runs
   // only when no other execute's DP is still in flight (a lone alignment's wall, not a pipeline's
-  // throughput: a second DP wants those CUs)
+  // throughput: a second DP wants those CUs) — on either DP stream, so every slot's last DP is
+  // asked; and only when the DP leaves a CU free
   bool conc = h->split && h->splitConc == 1;
   if (h->split && h->splitConc == 2) {
-    conc = true;
-    if (h->execCount > 0) {
-      const hipError_t q = hipEventQuery(h->slot[h->lastSlot].dpDone);
+    conc = h->shared() ? false : true;       // other handles' DPs are not visible here
+    for (int x = 0; x < h->depth && conc; ++x) {
+      if (!h->slot[x].inflight) continue;
+      const hipError_t q = hipEventQuery(h->slot[x].dpDone);
       if (q == hipErrorNotReady) conc = false;
       else BG_HIP(q);
     }
   }
+  if (h->cus - h->gridWgs <= 0) conc = false;
   // the previous user of this slot must have finished reading its trace
   if (S.inflight) BG_HIP(hipStreamWaitEvent(ds, S.finDone, 0));
+  // a shared handle's upload, not waited for by prepare
+  if (h->upPending) BG_HIP(hipStreamWaitEvent(ds, h->upDone, 0));
   hipEvent_t e[4] = {h->ev[0], h->ev[1], h->ev[2], h->ev[3]};
   if (h->profiling && h->ringUsed + 4 <= (int)h->ring.size()) {
     for (int x = 0; x < 4; ++x) e[x] = h->ring[h->ringUsed + x];
@@ -1314,10 +1423,10 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   // the third stream is created on first use: HIP maps a process's streams onto 4 hardware
   // queues round-robin, and an extra stream per handle moves other handles' copies behind
   // kernels in a shared queue (host_to_host runs four handles)
-  if (nfs == 3 && !h->stream4 && hipStreamCreateWithFlags(&h->stream4, hipStreamNonBlocking) != hipSuccess) {
-    h->stream4 = nullptr;
-    nfs = 2;
-  }
+  if (nfs >= 2 && !h->stream3) h->stream3 = group_stream(h, kSFin2);
+  if (nfs >= 2 && !h->stream3) nfs = 1;
+  if (nfs == 3 && !h->stream4) h->stream4 = group_stream(h, kSFin3);
+  if (nfs == 3 && !h->stream4) nfs = 2;
   const hipStream_t fss[3] = {h->stream2, h->stream3, h->stream4};
   hipStream_t fs = fss[h->execCount % nfs];
   // split traceback: its arguments, and the exit pass beside the DP (it waits for the DP's
@@ -1369,7 +1478,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       BG_HIP(hipFuncSetAttribute(cfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)clds));
       BG_HIP(hipStreamWaitEvent(fs, S.resetDone, 0));
       // one workgroup per CU the DP leaves free: even dispatched first, they leave the DP its CUs
-      const int cg = std::max(1, h->cus - h->gridWgs);
+      // (conc is off when the DP holds every CU)
+      const int cg = h->cus - h->gridWgs;
       BG_HIP(hipLaunchKernel(cfn, dim3(cg), dim3(h->R >= 8 ? 512 : 1024), cargs, clds, fs));
       X.conc = 0;
     }
@@ -1484,6 +1594,24 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   BG_HIP(hipEventRecord(e[3], fs));
   BG_HIP(hipEventRecord(S.finDone, fs));
   S.inflight = true;
+  // asynchronous fetch: the results' download queued behind the traceback, on a stream (and
+  // hardware queue) of its own, so it neither waits behind the next DPs nor delays the next
+  // tracebacks; bg_batch_fetch then finds the strings on the host
+  if (h->asyncFetch && np) {
+    if (!h->dlS) h->dlS = group_stream(h, kSDl);
+    if (!h->dlS) return BG_E_HIP;
+    if (!h->ho1.ensure(h->planOut + 1) || !h->ho2.ensure(h->planOut + 1) ||
+        !h->hresPin.ensure(sizeof(BgResult) * (np + 1)))
+      return BG_E_NOMEM;
+    BG_HIP(hipStreamWaitEvent(h->dlS, S.finDone, 0));
+    BG_HIP(hipMemcpyAsync(h->hresPin.p, S.results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, h->dlS));
+    if (h->planOut) {
+      BG_HIP(hipMemcpyAsync(h->ho1.p, S.out1.p, h->planOut, hipMemcpyDeviceToHost, h->dlS));
+      BG_HIP(hipMemcpyAsync(h->ho2.p, S.out2.p, h->planOut, hipMemcpyDeviceToHost, h->dlS));
+    }
+    BG_HIP(hipEventRecord(h->dlDone, h->dlS));
+    h->dlExec = h->execCount;
+  }
   if (e[0] != h->ev[0]) {  // keep the last execute's events for bg_get_stats
     h->last[0] = e[0]; h->last[1] = e[1]; h->last[2] = e[2]; h->last[3] = e[3];
   } else {
@@ -1497,12 +1625,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
 
 extern "C" int bg_synchronize(bg_aligner* h) {
   if (!h) return BG_E_ARG;
-  BG_HIP(hipSetDevice(h->device));
-  BG_HIP(hipStreamSynchronize(h->stream));
-  BG_HIP(hipStreamSynchronize(h->stream2));
-  BG_HIP(hipStreamSynchronize(h->stream3));
-  if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
-  if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
+  BG_HIP(drain(h));
   if (h->executed) {
     (void)hipEventElapsedTime(&h->dp_ms, h->last[0], h->last[1]);
     (void)hipEventElapsedTime(&h->fin_ms, h->last[2], h->last[3]);
@@ -1565,13 +1688,26 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   h->hres.resize(np);
   uint64_t ob = 0;
   for (const BgPair& P : h->plan) ob += (uint64_t)P.n1 + P.n2;
-  if (!h->ho1.ensure(ob + 1) || !h->ho2.ensure(ob + 1)) return BG_E_NOMEM;
-  if (np) {
-    const Slot& S = h->slot[h->lastSlot];
-    BG_HIP(hipMemcpyAsync(h->hres.data(), S.results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, h->stream));
-    BG_HIP(hipMemcpyAsync(h->ho1.p, S.out1.p, ob, hipMemcpyDeviceToHost, h->stream));
-    BG_HIP(hipMemcpyAsync(h->ho2.p, S.out2.p, ob, hipMemcpyDeviceToHost, h->stream));
-    BG_HIP(hipStreamSynchronize(h->stream));
+  if (h->asyncFetch && np && h->dlExec == h->execCount - 1) {
+    // downloaded behind the traceback (bg_set_async_fetch); the wait above covered it
+    std::memcpy(h->hres.data(), h->hresPin.p, sizeof(BgResult) * np);
+  } else {
+    if (!h->ho1.ensure(ob + 1) || !h->ho2.ensure(ob + 1)) return BG_E_NOMEM;
+    if (np) {
+      const Slot& S = h->slot[h->lastSlot];
+      // a handle sharing its streams downloads on the group's download stream (the DP stream
+      // holds other handles' DPs)
+      hipStream_t cs = h->stream;
+      if (h->shared()) {
+        if (!h->dlS) h->dlS = group_stream(h, kSDl);
+        if (!h->dlS) return BG_E_HIP;
+        cs = h->dlS;
+      }
+      BG_HIP(hipMemcpyAsync(h->hres.data(), S.results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, cs));
+      BG_HIP(hipMemcpyAsync(h->ho1.p, S.out1.p, ob, hipMemcpyDeviceToHost, cs));
+      BG_HIP(hipMemcpyAsync(h->ho2.p, S.out2.p, ob, hipMemcpyDeviceToHost, cs));
+      BG_HIP(hipStreamSynchronize(cs));
+    }
   }
   tm.mark(kPhFetchCopy, "fetch-d2h");
   for (size_t p = 0; p < h->npairs; ++p) {
@@ -1746,11 +1882,7 @@ extern "C" int bg_profile_begin(bg_aligner* h) {
 extern "C" int bg_profile_end(bg_aligner* h, float* avg_dp, float* avg_fin, int* n) {
   if (!h) return BG_E_ARG;
   BG_HIP(hipSetDevice(h->device));
-  BG_HIP(hipStreamSynchronize(h->stream));
-  BG_HIP(hipStreamSynchronize(h->stream2));
-  BG_HIP(hipStreamSynchronize(h->stream3));
-  if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
-  if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
+  BG_HIP(drain(h));
   double dp = 0, fin = 0;
   const int cnt = h->ringUsed / 4;
   for (int i = 0; i < cnt; ++i) {
@@ -1775,10 +1907,7 @@ extern "C" int bg_batch_export(bg_aligner* h, void* dst, size_t* bytes) {
   if (*bytes < need) return BG_E_ARG;
   if (!h->executed) return BG_E_NO_BATCH;
   BG_HIP(hipSetDevice(h->device));
-  BG_HIP(hipStreamSynchronize(h->stream2));
-  BG_HIP(hipStreamSynchronize(h->stream3));
-  if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
-  if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
+  BG_HIP(drain(h));
   const Slot& S = h->slot[h->lastSlot];
   const uint64_t n = h->npairs;
   BG_HIP(hipMemcpyAsync(dst, &n, 8, hipMemcpyHostToDevice, h->stream));
@@ -1823,10 +1952,7 @@ extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) 
     if (!h->compactSizes.ensure(8 * (n + 1))) return BG_E_NOMEM;
     E.sizes = h->compactSizes.as<uint64_t>();
     E.dst = nullptr;
-    BG_HIP(hipStreamSynchronize(h->stream2));
-    BG_HIP(hipStreamSynchronize(h->stream3));
-    if (h->stream4) BG_HIP(hipStreamSynchronize(h->stream4));
-    if (h->dps) BG_HIP(hipStreamSynchronize(h->dps));
+    BG_HIP(drain(h));
     BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), h->stream));
     const unsigned g = (unsigned)(((uint64_t)E.nplan + 255) / 256);
     if (g) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(g), dim3(256), args, 0, h->stream));

@@ -271,6 +271,41 @@ inline void call_history(size_t npairs, const size_t* n1, const size_t* n2,
   }
 }
 
+// ---- multi-device batches (bg_group, bg_group.cpp): a batch split over shards by cells,
+// largest pair first, each to the least-loaded shard (ties: the lower index), as
+// biogarden_amd/shard.py lpt_shards does for ranks.  shard_of[p] = the shard of pair p.
+inline void lpt_plan(size_t npairs, const size_t* n1, const size_t* n2, int nshards, int32_t* shard_of) {
+  std::vector<size_t> order(npairs);
+  for (size_t p = 0; p < npairs; ++p) order[p] = p;
+  std::stable_sort(order.begin(), order.end(), [&](size_t x, size_t y) {
+    return (uint64_t)n1[x] * n2[x] > (uint64_t)n1[y] * n2[y];
+  });
+  std::vector<uint64_t> load((size_t)std::max(nshards, 1), 0);
+  for (size_t p : order) {
+    int best = 0;
+    for (int r = 1; r < nshards; ++r)
+      if (load[r] < load[best]) best = r;
+    shard_of[p] = best;
+    load[best] += (uint64_t)n1[p] * n2[p];
+  }
+}
+
+// The scratch dims each call of a batch starts from, in caller order, for ONE reference aligner
+// running the whole batch (biogarden_amd/shard.py call_dims): the argument errors return before
+// the resize (aligner.rs:87-89, 153-155, 219-225), every other call resizes to (n1 + 1, n2 + 1)
+// when n1 > rows || n2 > cols (:92-94, 594-602).  rows / cols: in, the dims before the batch;
+// out, after it.
+inline void batch_call_dims(int mode, size_t npairs, const size_t* n1, const size_t* n2, int32_t a,
+                            int32_t b, long& rows, long& cols, std::vector<std::pair<long, long>>& dims) {
+  const bool badArgs = (mode == BG_GLOBAL || mode == BG_LOCAL || mode == BG_FITTING) && (a > 0 || b > 0);
+  dims.resize(npairs);
+  for (size_t p = 0; p < npairs; ++p) {
+    dims[p] = std::make_pair(rows, cols);
+    if (badArgs || (mode == BG_FITTING && n1[p] < n2[p])) continue;
+    if ((long)n1[p] > rows || (long)n2[p] > cols) { rows = (long)n1[p] + 1; cols = (long)n2[p] + 1; }
+  }
+}
+
 // ---- fetch: copy each pair's aligned strings from the downloaded slot buffers to the caller's
 // output, over the pool: job q copies len bytes at src of h1 / h2 to dst of out1 / out2.
 struct UnpackJob {
@@ -293,9 +328,12 @@ inline void unpack_strings(const std::vector<UnpackJob>& jobs, const uint8_t* h1
 // ---- the compact export record (include/biogarden_gpu.h bg_batch_export_compact) expanded on
 // the host into bg_batch_fetch's output, over the pool.  Every header is range-checked against
 // its pair before any byte is written; returns BG_OK or BG_E_ARG.
+// dstoff (np entries, or nullptr): where pair p's strings go in out1 / out2 (and its result's
+// offset); nullptr packs them back to back in pair order, as bg_batch_fetch does.
 inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uint8_t* const* s1,
                           const size_t* n1, const uint8_t* const* s2, const size_t* n2,
-                          bg_pair_result* res, uint8_t* out1, uint8_t* out2, size_t out_cap) {
+                          bg_pair_result* res, uint8_t* out1, uint8_t* out2, size_t out_cap,
+                          const uint64_t* dstoff = nullptr) {
   if (!rec || bytes < 32 || (np && (!res || !n1 || !n2 || !s1 || !s2))) return BG_E_ARG;
   uint64_t head[4];
   std::memcpy(head, rec, 32);
@@ -307,8 +345,14 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
   std::vector<bg_compact_hdr> hd(np);
   if (np) std::memcpy(hd.data(), rec + 32, np * sizeof(bg_compact_hdr));
   std::vector<uint64_t> off(np + 1, 0);
-  for (size_t p = 0; p < np; ++p) off[p + 1] = off[p] + n1[p] + n2[p];
-  if (off[np] && (!out1 || !out2 || out_cap < off[np])) return BG_E_ARG;
+  uint64_t end = 0;
+  for (size_t p = 0; p < np; ++p) {
+    off[p + 1] = off[p] + n1[p] + n2[p];
+    if (dstoff) off[p] = dstoff[p];
+    end = std::max<uint64_t>(end, off[p] + n1[p] + n2[p]);
+    if (dstoff && off[p] > (uint64_t)out_cap) return BG_E_ARG;
+  }
+  if (end && (!out1 || !out2 || out_cap < end)) return BG_E_ARG;
   for (size_t p = 0; p < np; ++p) {
     const bg_compact_hdr& h = hd[p];
     const uint64_t ncore = (uint64_t)h.len - h.npre - h.ntail;

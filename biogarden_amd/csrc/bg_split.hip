@@ -618,6 +618,14 @@ __global__ __launch_bounds__(256) void bg_exit_resolve_kernel(BgSplitArgs A) {
   const int tid = threadIdx.x;
   const int32_t* fr = ar + L.front + (size_t)s * L.G * F;
   int32_t* fs = ar + L.fres + (size_t)s * L.G * F;
+  // the start strip: the chain reads the resolved frontier of the segment before the capture
+  // segment head[5] only, and the exit pass stopped at the capture item (later segments' raw
+  // frontiers are stale) — resolve up to that segment
+  int GL = L.G;
+  if (s == sStar) {
+    const int cgs = ar[L.head + 5];
+    if (cgs >= 0 && cgs < L.G) GL = cgs + 1;   // (HEAD sets it to 0 before the pass: nothing to read)
+  }
   // The segments form a chain (segment g's symbols point into g - 1's resolved frontier), walked
   // by wave 0 alone: a wave's LDS operations complete in order, so a link costs its lookups, not
   // a workgroup barrier.  The raw frontiers do not depend on the chain: each lane keeps the raw
@@ -632,16 +640,16 @@ __global__ __launch_bounds__(256) void bg_exit_resolve_kernel(BgSplitArgs A) {
 #pragma unroll
       for (int q = 0; q < QW; ++q) {
         const int x = tid + 64 * q;
-        r[q] = (g + 1 < L.G && x < F) ? fr[(size_t)g * F + x] : 0;
+        r[q] = (g + 1 < GL && x < F) ? fr[(size_t)g * F + x] : 0;
       }
     };
 #pragma unroll
     for (int d = 0; d < D; ++d) fetch(1 + d, raw[d]);
-    for (int g0 = 1; g0 + 1 < L.G; g0 += D) {
+    for (int g0 = 1; g0 + 1 < GL; g0 += D) {
 #pragma unroll
       for (int d = 0; d < D; ++d) {
         const int g = g0 + d;
-        if (g + 1 >= L.G) break;                         // wave-uniform
+        if (g + 1 >= GL) break;                         // wave-uniform
 #pragma unroll
         for (int q = 0; q < QW; ++q) {
           const int x = tid + 64 * q;

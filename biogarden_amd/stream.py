@@ -1,12 +1,19 @@
 """Streaming batch alignment on one GPU: FASTA -> packed residues -> HBM, overlapped with the
 kernels.
 
-`AlignStream` keeps a rotation of handles (`bg_aligner`, each with its own HIP streams and
-arenas).  Submitting batch k stages its residues in pinned memory and queues its upload and
-kernels on handle k mod H while batches k-1 .. k-H+1 are still on the GPU; the oldest batch is
-fetched (D2H of the aligned strings into host buffers) only when its handle comes round again.
-The host's byte passes, the PCIe copies and the kernels of different batches therefore overlap,
-and the GPU sees a steady queue of batches (bench.py's `host_to_host` leg measures it).
+`AlignStream` keeps a rotation of handles (`bg_aligner`, each with its own arenas and batch).
+Submitting batch k stages its residues in pinned memory and queues its upload and kernels on
+handle k mod H while batches k-1 .. k-H+1 are still on the GPU; the oldest batch is collected
+(its aligned strings unpacked into host buffers) only when its handle comes round again.
+
+The handles share ONE set of HIP streams (`bg_aligner_new_shared`): uploads, DPs, tracebacks and
+downloads, four hardware queues in all, so no copy waits in a queue behind another batch's
+kernel (the MI355X boxes give a process 4 queues, GPU_MAX_HW_QUEUES).  The DPs of consecutive
+batches run back to back on the DP stream with each traceback beside the next DP, as one
+handle's executes do, and every execute queues its strings' download right behind its traceback
+(`bg_set_async_fetch`).  The host's byte passes, the PCIe copies and the kernels of different
+batches therefore overlap, and the GPU sees a steady queue of batches (bench.py's
+`host_to_host` leg measures it).
 
     with AlignStream("semiglobal", score.blosum62, -1, -2) as st:
         for reads in fasta.BatchReader("reads.fa", max_records=8192):
@@ -30,17 +37,25 @@ from .ds.sequence import Sequence
 
 
 class AlignStream:
-    def __init__(self, mode, score, a, b, device=0, handles=4, pipeline=3, raw=False):
+    def __init__(self, mode, score, a, b, device=0, handles=4, pipeline=2, raw=False,
+                 shared=True):
         """raw=True: results are Handle.fetch_raw() records (status / score / offset / len
         lists and the two string buffers, valid until the same handle is collected again)
-        instead of AlignmentResult objects — for throughput measurement (bench.py)."""
+        instead of AlignmentResult objects — for throughput measurement (bench.py).
+        pipeline: each handle's slots (>= 2 plans the DP with room for the traceback beside it,
+        which the rotation puts there).  shared=False: every handle on streams of its own (the
+        round-4 layout, kept for comparison)."""
         if handles < 1:
             raise ValueError("handles must be >= 1")
         self.raw = raw
         self.mode, self.score, self.a, self.b = mode, score, int(a), int(b)
-        self._hs = [_native.Handle(device) for _ in range(handles)]
+        first = _native.Handle(device)
+        self._hs = [first] + [_native.Handle(device, share=first if shared else None)
+                              for _ in range(handles - 1)]
         for h in self._hs:
             h.set_pipeline(pipeline)
+            if shared:
+                h.set_async_fetch(True)
         self._next = 0
         self._inflight = deque()            # (handle index, tag, panics, pairs-or-None)
         # batches collected to free a handle whose submit then failed (prepare / execute raised):

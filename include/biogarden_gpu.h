@@ -84,7 +84,20 @@ typedef struct bg_aligner bg_aligner;
 
 /* device: HIP device ordinal (one process per GPU).  NULL on failure. */
 bg_aligner* bg_aligner_new(int device);
+/* A second aligner on peer's device that shares peer's HIP streams: several handles holding
+ * different batches in flight (the streaming rotation of biogarden_amd/stream.py, one reference
+ * SequenceAligner fed batch after batch) then use four streams in all — uploads, DPs,
+ * tracebacks, downloads — and so four hardware queues, whatever the number of handles.  The DPs
+ * and tracebacks of consecutive batches pipeline as one handle's executes do.  Each handle keeps
+ * its own arenas and batch; waits (prepare, fetch, synchronize) wait for the handle's own work
+ * only.  The streams live until the last handle sharing them is freed.  NULL on failure. */
+bg_aligner* bg_aligner_new_shared(bg_aligner* peer);
 void bg_aligner_free(bg_aligner* h);
+/* on != 0: every bg_batch_execute also queues the download of its results (scores, both
+ * aligned strings) into the handle's pinned host buffers, on a stream of its own right after the
+ * traceback; bg_batch_fetch then waits for that download and unpacks it, with no copy of its own.
+ * For callers that fetch every execute (the streaming rotation).  Default 0. */
+int bg_set_async_fetch(bg_aligner* h, int on);
 
 /* One alignment.  out1/out2 receive the aligned strings ('-' for gaps), both *out_len bytes;
  * cap must be >= n1 + n2.  Returns a BG_* status (>= 0) or a BG_E_* error (< 0). */
@@ -225,6 +238,38 @@ int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes);
 int bg_compact_expand(const void* rec, size_t rec_bytes, size_t npairs, const uint8_t* const* s1,
                       const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                       bg_pair_result* results, uint8_t* out1, uint8_t* out2, size_t out_cap);
+
+/* ---- Several GPUs from one process: the batched SequenceAligner call over a Tile
+ * (aligner.rs:84-435, ds/tile.rs:9-11; as tests/integration.rs:234-312 and
+ * examples/from_file.rs:19-32 call it) spread over the node's devices.
+ * bg_group_new: one aligner per entry of devices[0..n) (a device may repeat: several shards on one
+ * GPU, which then share its streams) and one RCCL communicator over the distinct devices
+ * (ncclCommInitAll; librccl is loaded at this call).  NULL on failure (no device, no librccl).
+ * bg_group_align_batch: bg_align_batch's contract over the group — the pairs are split over the
+ * members by cells (largest first, to the least-loaded member; bg_group_plan), every member aligns
+ * its shard and packs the compact record on its device (bg_batch_export_compact), the records are
+ * gathered to the first member's device (RCCL send / recv over xGMI; a device copy for members on
+ * that device) and downloaded once, and the host expands them into out1 / out2 at the offsets
+ * bg_align_batch uses.  The group stands for ONE reference aligner: every pair's status 4 is judged
+ * against the scratch dims that aligner would have after the pairs before it in caller order
+ * (bg_group_buffer_size; aligner.rs:92-94, 594-602).  Results are identical to bg_align_batch on
+ * one aligner fed the same batches. */
+typedef struct bg_group bg_group;
+bg_group* bg_group_new(const int* devices, int n);
+void bg_group_free(bg_group* g);
+int bg_group_size(const bg_group* g);
+/* member m's aligner (for bg_get_stats and the like), owned by the group */
+bg_aligner* bg_group_member(bg_group* g, int m);
+int bg_group_align_batch(bg_group* g, int mode, size_t npairs, const uint8_t* const* s1,
+                         const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                         const bg_scoring* scoring, int32_t a, int32_t b, bg_pair_result* results,
+                         uint8_t* out1, uint8_t* out2, size_t out_cap);
+/* Host-only: the group's split of a batch over nshards (shard_of[p] for every pair). */
+int bg_group_plan(size_t npairs, const size_t* n1, const size_t* n2, int nshards, int32_t* shard_of);
+int bg_group_buffer_size(bg_group* g, size_t* rows, size_t* cols);
+/* Accumulated ms per phase of bg_group_align_batch: [0] prepare + execute, [1] the members'
+ * waits and exports, [2] the gather, [3] the download, [4] the expansion; *calls the call count. */
+int bg_group_timing(bg_group* g, double* ms, size_t n, uint64_t* calls, int reset);
 
 /* Host-side time of this handle's bg_batch_prepare / bg_batch_fetch calls, accumulated (ms):
  *   ms[0] waiting for the handle's previous work   ms[1] validation + staging (byte pass)

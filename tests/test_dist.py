@@ -282,3 +282,20 @@ def test_call_dims_follow_the_reference_aligner(mode, a, b):
     idx = [3, 0, 17, 9]
     assert shard.shard_call_dims(mode, [(len(x), len(y)) for x, y in pairs], a, b, idx) == \
         [want[p] for p in idx]
+
+
+def test_group_plan_matches_rank_sharding():
+    """bg_group_plan (the C ABI's multi-device split, host-only) assigns every pair to the shard
+    shard.lpt_shards gives it: the single-process group and the one-process-per-GPU ranks split a
+    batch the same way."""
+    import random
+    from biogarden_amd import _native, shard
+    rng = random.Random(8)
+    for _ in range(40):
+        n = rng.randint(0, 400)
+        k = rng.randint(1, 9)
+        sizes = [(rng.choice([0, 1, 150, 1000, rng.randint(0, 9000)]),
+                  rng.choice([0, 10, 10000, rng.randint(0, 9000)])) for _ in range(n)]
+        got = _native.group_plan(sizes, k)
+        want = shard.lpt_shards(sizes, k)
+        assert [[p for p in range(n) if got[p] == r] for r in range(k)] == want

@@ -165,3 +165,28 @@ def test_split_pipelined_two_dp_streams(oracle, monkeypatch, depth, conc):
         h.close()
     _check(oracle, "semiglobal", pairs, got, -1, -2)
     assert sp["tail_moves"] == 0, sp
+
+
+def test_split_arena_reused_across_layouts(oracle):
+    """One handle prepares a large split batch, then a smaller one with another layout (other
+    lengths, strips and segments): the split arena is zeroed at every prepare, so no column
+    number of the first batch can stand where the second one's epoch tags live — the strip walks
+    still cover the whole traceback (a stale int equal to the epoch skipped items)."""
+    from biogarden_amd import _native
+    rng = random.Random(4242)
+    big = _pairs(rng, [(16000, 15000), (9000, 12000)])
+    small = _pairs(rng, [(7000, 5000), (5200, 3100), (3000, 6000)])
+    sc = _native.builtin_scoring(_native.BG_BLOSUM62)
+    h = _native.Handle(0)
+    try:
+        for pairs, reps in ((big, 2), (small, 3), (big[:1], 1)):
+            h.prepare("semiglobal", pairs, sc, -1, -2)
+            for _ in range(reps):
+                h.execute()
+            got = h.fetch()
+            _check(oracle, "semiglobal", pairs, got, -1, -2)
+            assert h.stats()["split"] == 1
+            sp = h.split_stats()
+            assert sp["pairs_overflow"] == 0 and sp["tail_moves"] == 0, sp
+    finally:
+        h.close()

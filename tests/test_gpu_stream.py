@@ -100,3 +100,82 @@ def test_failed_submit_keeps_collected_results(oracle):
     assert [t for t, _ in seen] == [0, 1, 3]
     for t, res in seen:
         check_results(oracle, "global", batches[t], res, "blosum62", -11, -1)
+
+
+def test_shared_stream_handles_hold_independent_batches(oracle):
+    """Handles sharing one stream set (bg_aligner_new_shared) hold different batches in flight at
+    once: every fetch waits for its own handle's work only, in any order; an asynchronous fetch
+    (bg_set_async_fetch, the download queued behind the traceback) returns what a plain fetch
+    returns, also after several executes of one batch."""
+    from biogarden_amd import _native
+    rng = random.Random(99)
+    jobs = [("global", -11, -1), ("semiglobal", -1, -2), ("local", -11, -1), ("overlap", -2, -3)]
+    batches = []
+    for _ in jobs:
+        pairs = []
+        for _ in range(rng.randint(20, 60)):
+            s1 = rand_seq(rng, rng.randint(0, 2500), DNA)
+            pairs.append((s1, mutate(rng, s1, DNA, 0.12)[: rng.randint(0, 2600)]))
+        batches.append(pairs)
+    sc = _native.builtin_scoring(_native.BG_BLOSUM62)
+    first = _native.Handle(0)
+    hs = [first] + [_native.Handle(share=first) for _ in jobs[1:]]
+    try:
+        for k, h in enumerate(hs):
+            h.set_pipeline(1 + k % 3)
+            if k % 2:
+                h.set_async_fetch(True)
+        for h, (mode, a, b), pairs in zip(hs, jobs, batches):
+            h.prepare(mode, pairs, sc, a, b)
+            h.execute()
+        for k in (2, 0, 3, 1):
+            mode, a, b = jobs[k]
+            got = hs[k].fetch()
+            check_results(oracle, mode, batches[k], [_res(r) for r in got], "blosum62", a, b,
+                          dims=(1024, 1024))
+        # several executes of one batch in flight beside another handle's, then one fetch
+        hs[1].execute()
+        hs[3].execute()
+        hs[1].execute()
+        hs[1].execute()
+        again = hs[1].fetch()
+        first_run = hs[3].fetch()
+        mode, a, b = jobs[1]
+        check_results(oracle, mode, batches[1], [_res(r) for r in again], "blosum62", a, b,
+                      dims=(1024, 1024))
+        mode, a, b = jobs[3]
+        check_results(oracle, mode, batches[3], [_res(r) for r in first_run], "blosum62", a, b,
+                      dims=(1024, 1024))
+    finally:
+        for h in reversed(hs):
+            h.close()
+
+
+def _res(r):
+    from biogarden_amd.alignment.aligner import AlignmentResult
+    from biogarden_amd.ds.sequence import Sequence
+    return AlignmentResult(r["score"], Sequence(r["aligned1"]), Sequence(r["aligned2"]), r["status"],
+                           r["end"], r["start"])
+
+
+@pytest.mark.parametrize("shared", [True, False])
+def test_stream_shared_and_unshared_agree(oracle, shared):
+    """The rotation on one shared stream set with asynchronous downloads (the default) and on
+    streams of its own per handle give the same results, batch for batch."""
+    from biogarden_amd.alignment import score
+    from biogarden_amd.stream import AlignStream
+    rng = random.Random(5)
+    batches = []
+    for t in range(6):
+        pairs = [(rand_seq(rng, rng.randint(100, 3000), DNA), rand_seq(rng, rng.randint(100, 3000), DNA))
+                 for _ in range(rng.randint(1, 30))]
+        batches.append(pairs)
+    out = []
+    with AlignStream("semiglobal", score.blosum62, -1, -2, handles=3, shared=shared) as st:
+        for t, pairs in enumerate(batches):
+            out += st.submit(pairs, tag=t)
+        out += st.drain()
+    assert [t for t, _ in out] == list(range(6))
+    ref = oracle.Aligner(dims=(1024, 1024))
+    for (t, res), pairs in zip(out, batches):
+        check_results(oracle, "semiglobal", pairs, res, "blosum62", -1, -2, ref=ref)
