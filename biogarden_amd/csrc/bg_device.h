@@ -298,6 +298,17 @@ struct BgCompactArgs {
   int32_t mode;
 };
 
+// bg_download_kernel (bg_io.hip): up to three device -> host-mapped copies
+struct BgDownloadSeg {
+  const uint8_t* src;      // device
+  uint8_t* dst;            // host-mapped pinned memory (hipHostGetDevicePointer)
+  uint64_t bytes;
+};
+struct BgDownloadArgs {
+  BgDownloadSeg seg[3];
+  int32_t nseg;
+};
+
 struct BgExportArgs {
   const BgPair* pairs;
   const BgResult* results;

@@ -21,22 +21,11 @@
 #ifndef BG_SEQCHECK
 #define BG_SEQCHECK 0      // verification builds: the walker re-checks its decode (reanchor)
 #endif
-#ifndef BG_FIN_WAKEUP
-#define BG_FIN_WAKEUP 0
-#endif
 #ifndef BG_HELP_LONG
 #define BG_HELP_LONG 8
 #endif
-// the helpers' pauses: s_sleep, or (BG_FIN_NOSLEEP, s_wakeup diagnosis) busy s_nops, so that no
-// wave of the workgroup is ever in s_sleep
-#ifndef BG_FIN_NOSLEEP
-#define BG_FIN_NOSLEEP 0
-#endif
-#define help_pause(n)                                                   \
-  do {                                                                  \
-    if constexpr (BG_FIN_NOSLEEP) asm volatile("s_nop 7\n\ts_nop 7"); \
-    else __builtin_amdgcn_s_sleep(n);                                   \
-  } while (0)
+// the helpers' pauses (the walker never wakes them: DESIGN §4.4, s_wakeup)
+#define help_pause(n) __builtin_amdgcn_s_sleep(n)
 #include "bg_device.h"
 #include "bg_tag_common.h"
 
@@ -1031,17 +1020,6 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
               __hip_atomic_store(&sh[35], l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
               __hip_atomic_store(&sh[33], key, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
-#if BG_FIN_WAKEUP == 1
-            // experiment (round 2's failing variant, re-created for diagnosis): wake the sleeping
-            // helpers of this workgroup right after posting the request
-            asm volatile("s_wakeup" ::: "memory");
-#elif BG_FIN_WAKEUP == 2
-            asm volatile("s_nop 0" ::: "memory");             // the same statement, no wakeup
-#elif BG_FIN_WAKEUP == 3
-            asm volatile("s_wakeup");                         // the wakeup, no memory clobber
-#elif BG_FIN_WAKEUP == 4
-            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_wakeup" ::: "memory");   // after every access
-#endif
             const unsigned* me = &ckMap[ck_map_idx(reqS, reqB0)];
             // Forward progress: after kSelfPolls polls without a helper taking the request (all
             // busy prefetching), the walker claims a slot under the same lock and recomputes the
@@ -1168,9 +1146,6 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       if (lane == 0) { sh[4] = reqS; sh[5] = reqB0; sh[6] = done; sh[11] = crossed; }
       if (ballot(wild) && lane == 0) sh[9] = 5;                // BG_INTERNAL: see put_op
       if (async && lane == 0) __hip_atomic_store(&sh[32], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#if BG_FIN_WAKEUP == 5
-      if (async) asm volatile("s_wakeup" ::: "memory");       // once, as the walk ends (diagnosis)
-#endif
     }
     __syncthreads();
     done = sh[6];

@@ -50,6 +50,7 @@ extern "C" void* bg_compact_size_kernel_ptr();
 extern "C" void* bg_compact_scan_kernel_ptr();
 extern "C" void* bg_compact_write_kernel_ptr();
 extern "C" void* bg_code_kernel_ptr();
+extern "C" void* bg_download_kernel_ptr();
 extern "C" void* bg_global_score_kernel_ptr();
 extern "C" void* bg_dp_aff_kernel_ptr(int R, int local);
 extern "C" int bg_dp_aff_head_bytes(void);
@@ -98,9 +99,16 @@ struct PinBuf {
     p = nullptr;
     cap = 0;
     const size_t want = std::max<size_t>(bytes + bytes / 4, 1 << 16);
-    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) { p = nullptr; return false; }
+    if (hipHostMalloc(&p, want, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) { p = nullptr; return false; }
     cap = want;
+    dev = nullptr;
     return true;
+  }
+  // the address kernels write through (bg_download_kernel)
+  void* dev = nullptr;
+  void* device_ptr() {
+    if (!dev && p && hipHostGetDevicePointer(&dev, p, 0) != hipSuccess) dev = nullptr;
+    return dev;
   }
   void release() {
     if (p) (void)hipHostFree(p);
@@ -111,6 +119,13 @@ struct PinBuf {
 };
 
 inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
+
+// bg_download_kernel's grid: enough 256-thread blocks to keep PCIe busy, few enough to sit
+// beside the next DP (no LDS, a handful of VGPRs); BG_DL_BLOCKS overrides
+static const unsigned kDownloadBlocks = [] {
+  const char* e = std::getenv("BG_DL_BLOCKS");
+  return e ? (unsigned)std::max(1, std::atoi(e)) : 64u;
+}();
 
 // Host-side phases of prepare / fetch, accumulated per handle (bg_host_timing) and, with
 // BG_PREPARE_TIMING set, printed per call on stderr
@@ -1310,10 +1325,40 @@ extern "C" int bg_batch_prepare_table(bg_aligner* h, int mode, size_t npairs,
   return prepare_impl(h, mode, npairs, s1, n1, s2, n2, S, a, b);
 }
 
+namespace {
+// BG_EXEC_TIMING: the whole call, entry to return (stderr)
+struct CallClock {
+  const char* what;
+  bool on;
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  CallClock(const char* w, bool o) : what(w), on(o) {}
+  ~CallClock() {
+    if (on)
+      std::fprintf(stderr, "%s total %.3f ms\n", what,
+                   std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  }
+};
+}  // namespace
+
 extern "C" int bg_batch_execute(bg_aligner* h) {
+  static const bool callTiming = std::getenv("BG_EXEC_TIMING") != nullptr;
+  CallClock clk("execute", callTiming);
   if (!h) return BG_E_ARG;
   if (!h->prepared) return BG_E_NO_BATCH;
+  // BG_EXEC_TIMING: host time of this call's steps on stderr (which HIP call blocks)
+  static const bool exTiming = std::getenv("BG_EXEC_TIMING") != nullptr;
+  auto exT = std::chrono::steady_clock::now();
+  char exBuf[256];
+  int exN = 0;
+  auto exMark = [&](const char* what) {
+    if (!exTiming) return;
+    const auto now = std::chrono::steady_clock::now();
+    exN += std::snprintf(exBuf + exN, sizeof(exBuf) - exN > 0 ? sizeof(exBuf) - exN : 0, " %s %.3f", what,
+                         std::chrono::duration<double, std::milli>(now - exT).count());
+    exT = now;
+  };
   BG_HIP(hipSetDevice(h->device));
+  exMark("setdev");
   const unsigned np = (unsigned)h->plan.size();
   const int z = h->execCount % h->depth;
   Slot& S = h->slot[z];
@@ -1347,6 +1392,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   if (S.inflight) BG_HIP(hipStreamWaitEvent(ds, S.finDone, 0));
   // a shared handle's upload, not waited for by prepare
   if (h->upPending) BG_HIP(hipStreamWaitEvent(ds, h->upDone, 0));
+  exMark("waits");
   hipEvent_t e[4] = {h->ev[0], h->ev[1], h->ev[2], h->ev[3]};
   if (h->profiling && h->ringUsed + 4 <= (int)h->ring.size()) {
     for (int x = 0; x < 4; ++x) e[x] = h->ring[h->ringUsed + x];
@@ -1405,10 +1451,13 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     void* args[] = {&A};
     if (h->lds > 65536)
       BG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds));
+    exMark("dp-attr");
     BG_HIP(hipLaunchKernel(fn, dim3(h->gridWgs), dim3(64 * h->W), args, h->lds, ds));
   }
+  exMark("dp");
   BG_HIP(hipEventRecord(e[1], ds));
   BG_HIP(hipEventRecord(S.dpDone, ds));
+  exMark("dp-events");
   // The traceback stream.  A WIDE batch (a few long pairs: C3) is traceback-bound and its walks
   // occupy a handful of CUs, so consecutive executes' tracebacks alternate between two streams
   // and run side by side (each still waits for its own DP; the slot it reads is not reused before
@@ -1591,9 +1640,11 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
                              bg_finish_lds_bytes(F.win_bytes), fs));
     }
   }
+  exMark("finish");
   BG_HIP(hipEventRecord(e[3], fs));
   BG_HIP(hipEventRecord(S.finDone, fs));
   S.inflight = true;
+  exMark("fin-events");
   // asynchronous fetch: the results' download queued behind the traceback, on a stream (and
   // hardware queue) of its own, so it neither waits behind the next DPs nor delays the next
   // tracebacks; bg_batch_fetch then finds the strings on the host
@@ -1603,15 +1654,38 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     if (!h->ho1.ensure(h->planOut + 1) || !h->ho2.ensure(h->planOut + 1) ||
         !h->hresPin.ensure(sizeof(BgResult) * (np + 1)))
       return BG_E_NOMEM;
+    exMark("dl-ensure");
     BG_HIP(hipStreamWaitEvent(h->dlS, S.finDone, 0));
-    BG_HIP(hipMemcpyAsync(h->hresPin.p, S.results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, h->dlS));
-    if (h->planOut) {
-      BG_HIP(hipMemcpyAsync(h->ho1.p, S.out1.p, h->planOut, hipMemcpyDeviceToHost, h->dlS));
-      BG_HIP(hipMemcpyAsync(h->ho2.p, S.out2.p, h->planOut, hipMemcpyDeviceToHost, h->dlS));
+    exMark("dl-wait");
+    // the download as a kernel writing the host-mapped buffers (bg_io.hip): the copy-engine form
+    // (BG_DL_COPY=1) can block this call for several ms in PyTorch's HIP runtime
+    static const bool dlCopy = std::getenv("BG_DL_COPY") != nullptr;
+    void* dres = h->hresPin.device_ptr();
+    void* d1 = h->ho1.device_ptr();
+    void* d2 = h->ho2.device_ptr();
+    if (!dlCopy && dres && d1 && d2) {
+      BgDownloadArgs D;
+      std::memset(&D, 0, sizeof(D));
+      D.seg[0] = {S.results.as<uint8_t>(), static_cast<uint8_t*>(dres), sizeof(BgResult) * np};
+      D.seg[1] = {S.out1.as<uint8_t>(), static_cast<uint8_t*>(d1), (uint64_t)h->planOut};
+      D.seg[2] = {S.out2.as<uint8_t>(), static_cast<uint8_t*>(d2), (uint64_t)h->planOut};
+      D.nseg = 3;
+      const uint64_t vec = (2 * (uint64_t)h->planOut + sizeof(BgResult) * np) / 16;
+      const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(kDownloadBlocks, (vec + 255) / 256));
+      void* dargs[] = {&D};
+      BG_HIP(hipLaunchKernel(bg_download_kernel_ptr(), dim3(blocks), dim3(256), dargs, 0, h->dlS));
+    } else {
+      BG_HIP(hipMemcpyAsync(h->hresPin.p, S.results.p, sizeof(BgResult) * np, hipMemcpyDeviceToHost, h->dlS));
+      if (h->planOut) {
+        BG_HIP(hipMemcpyAsync(h->ho1.p, S.out1.p, h->planOut, hipMemcpyDeviceToHost, h->dlS));
+        BG_HIP(hipMemcpyAsync(h->ho2.p, S.out2.p, h->planOut, hipMemcpyDeviceToHost, h->dlS));
+      }
     }
     BG_HIP(hipEventRecord(h->dlDone, h->dlS));
     h->dlExec = h->execCount;
+    exMark("download");
   }
+  if (exTiming && exN) std::fprintf(stderr, "execute ms:%s\n", exBuf);
   if (e[0] != h->ev[0]) {  // keep the last execute's events for bg_get_stats
     h->last[0] = e[0]; h->last[1] = e[1]; h->last[2] = e[2]; h->last[3] = e[3];
   } else {

@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -353,7 +354,10 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
     if (dstoff && off[p] > (uint64_t)out_cap) return BG_E_ARG;
   }
   if (end && (!out1 || !out2 || out_cap < end)) return BG_E_ARG;
-  for (size_t p = 0; p < np; ++p) {
+  // every pair checked (over the pool) before any byte is written
+  std::atomic<int> fail{BG_OK};
+  par_ranges(np, [&](size_t p) -> uint64_t { return hd[p].len / 4 + 64; }, [&](size_t lo, size_t hi) {
+  for (size_t p = lo; p < hi && fail.load(std::memory_order_relaxed) == BG_OK; ++p) {
     const bg_compact_hdr& h = hd[p];
     const uint64_t ncore = (uint64_t)h.len - h.npre - h.ntail;
     // BG_COMPACT_DEBUG: name the record that fails a check (stderr)
@@ -362,28 +366,45 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
         std::fprintf(stderr, "compact_expand: pair %zu check %d: status %u len %u npre %u ntail %u start %u %u end %u %u n %zu %zu\n",
                      p, why, (unsigned)h.status, (unsigned)h.len, (unsigned)h.npre, (unsigned)h.ntail,
                      (unsigned)h.start1, (unsigned)h.start2, (unsigned)h.end_i, (unsigned)h.end_j, n1[p], n2[p]);
-      return BG_E_ARG;
+      fail.store(BG_E_ARG, std::memory_order_relaxed);
     };
     if ((uint64_t)h.npre + h.ntail > h.len || h.len > n1[p] + n2[p] || h.ops_off + (ncore + 3) / 4 > opsBytes ||
         h.start1 > n1[p] || h.start2 > n2[p] || h.end_i > n1[p] || h.end_j > n2[p] ||
-        (n1[p] && !s1[p]) || (n2[p] && !s2[p]))
-      return bad(1);
-    // the core consumes exactly s1[start1, end_i) and s2[start2, end_j)
+        (n1[p] && !s1[p]) || (n2[p] && !s2[p])) {
+      bad(1);
+      continue;
+    }
+    // the core consumes exactly s1[start1, end_i) and s2[start2, end_j): op 0 (diagonal) takes
+    // both, 1 (up) s1 only, 2 (left) s2 only, 3 is invalid — counted 32 ops per 64-bit word from
+    // the ops' low and high bit planes
     uint64_t c1 = 0, c2 = 0;
-    for (uint64_t x = 0; x < ncore; ++x) {
-      const int op = (ops[h.ops_off + x / 4] >> (2 * (x % 4))) & 3;
-      if (op == 3) return bad(2);
+    bool three = false;
+    const uint8_t* po = ops + h.ops_off;
+    const uint64_t kLo = 0x5555555555555555ull;
+    uint64_t x = 0;
+    for (; x + 32 <= ncore; x += 32) {
+      uint64_t w;
+      std::memcpy(&w, po + x / 4, 8);
+      const uint64_t lo = w & kLo, hi = (w >> 1) & kLo;
+      three |= (lo & hi) != 0;
+      c1 += 32 - (uint64_t)__builtin_popcountll(hi);
+      c2 += 32 - (uint64_t)__builtin_popcountll(lo);
+    }
+    for (; x < ncore; ++x) {
+      const int op = (po[x / 4] >> (2 * (x % 4))) & 3;
+      three |= op == 3;
       c1 += op != 2;
       c2 += op != 1;
     }
-    if (h.start1 + c1 != h.end_i || h.start2 + c2 != h.end_j) return bad(3);
+    if (three) { bad(2); continue; }
+    if (h.start1 + c1 != h.end_i || h.start2 + c2 != h.end_j) { bad(3); continue; }
     // the reference's semiglobal assembly (aligner.rs:389-428): the tail gap columns run from the
     // end cell to the last row / column, and a walk that returned (status 0) is preceded by the
     // prefix of the sequence it stopped in, exactly up to its start cell (row case: s2[0, start2),
     // column case: s1[0, start1)); the other modes have neither
     const bool colcase = h.end_i < n1[p];
     if (!semi) {
-      if (h.npre || h.ntail) return bad(4);
+      if (h.npre || h.ntail) bad(4);
     } else {
       const uint64_t tail = colcase ? n1[p] - h.end_i : n2[p] - h.end_j;
       const uint64_t pre = colcase ? h.start1 : h.start2;
@@ -392,9 +413,11 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
       const bool whole = h.npre == pre && h.ntail == tail;
       const bool stopped = h.npre == 0 && (h.ntail == 0 || h.ntail == tail);
       if (h.status == 0 ? !whole : h.status == BG_REF_DIVERGENT ? !(whole || stopped) : !stopped)
-        return bad(5);
+        bad(5);
     }
   }
+  });
+  if (fail.load() != BG_OK) return fail.load();
   par_ranges(np, [&](size_t p) -> uint64_t { return 2ull * hd[p].len + 64; }, [&](size_t lo, size_t hi) {
     for (size_t p = lo; p < hi; ++p) {
       const bg_compact_hdr& h = hd[p];

@@ -1,0 +1,5 @@
+#!/bin/bash
+set -o pipefail
+out=gpurun_out/r05/${1:-execp}
+mkdir -p $out
+H2H_PROFILE=1 timeout -k 10 300 python -u tools/r05/h2h_probe.py --handles 4 --rounds 12 --torch > $out/p_torch.jsonl 2> $out/p_torch.err
