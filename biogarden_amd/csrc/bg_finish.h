@@ -45,10 +45,8 @@ struct Fin {
   const int32_t* lastcol;     // M(i, n2)
 };
 
-__device__ __forceinline__ int lastrowM(const Fin& f, int j) {
-  if (f.n1 == 0) return row0_M(f.mode, j, f.a, f.b);
-  if (j == 0) return col0_M(f.mode, f.n1, f.a, f.b);
-  const int v = f.lastrowMa[j];
+// M(n1, j), j >= 1, from the last strip's stored row value v = lastrowMa[j]
+__device__ __forceinline__ int lastrow_from(const Fin& f, int v, int j) {
   // the tagged kernel stores X forms 4*(M(n1,j) - a*(n1+j)) + 2
   // checkpoint mode (tag 2) stores M'(n1,j) = M(n1,j) - a*(n1+j) itself
   if (f.F->tag == 2) return wadd(v, wmul(f.a, f.n1 + j));
@@ -56,6 +54,13 @@ __device__ __forceinline__ int lastrowM(const Fin& f, int j) {
   if (f.F->tag == 3) return wadd(wadd(v, -wadd(f.a, -f.b)), wmul(f.b, f.n1 + j));
   return f.F->tag ? wadd(v >> 2, wmul(f.a, f.n1 + j)) : wadd(v, -f.a);
 }
+__device__ __forceinline__ int lastrowM(const Fin& f, int j) {
+  if (f.n1 == 0) return row0_M(f.mode, j, f.a, f.b);
+  if (j == 0) return col0_M(f.mode, f.n1, f.a, f.b);
+  return lastrow_from(f, f.lastrowMa[j], j);
+}
+// end-cell folds: loads in flight per thread
+constexpr int kEndU = 8;
 __device__ __forceinline__ int lastcolM(const Fin& f, int i) {
   if (f.n2 == 0) return col0_M(f.mode, i, f.a, f.b);
   if (i == 0) return row0_M(f.mode, f.n2, f.a, f.b);
@@ -353,17 +358,49 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         }
       }
     } else if (mode == BGK_FITTING || mode == BGK_SEMIGLOBAL) {
-#pragma unroll 4
-      for (int i = tid; i <= n1; i += NT) {          // last column, first strict max (:247, :376)
-        const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
-        ka = kk > ka ? kk : ka;
+      // last column, first strict max (:247, :376); the border cell (i = 0) apart, then kEndU
+      // loads in flight per thread (one load per pass serialised C4's 10 k-column row fold:
+      // ~105 k cycles per pair before the walk)
+      if (tid == 0) ka = ((u64)bias(lastcolM(f, 0)) << 32) | 0xFFFFFFFFu;
+      if (n2 == 0) {
+        for (int i = 1 + tid; i <= n1; i += NT) {
+          const u64 kk = ((u64)bias(lastcolM(f, i)) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+          ka = kk > ka ? kk : ka;
+        }
+      } else {
+        for (int i0 = 1 + tid; i0 <= n1; i0 += NT * kEndU) {
+          int v[kEndU];
+#pragma unroll
+          for (int u = 0; u < kEndU; ++u) v[u] = i0 + u * NT <= n1 ? f.lastcol[i0 + u * NT] : 0;
+#pragma unroll
+          for (int u = 0; u < kEndU; ++u) {
+            const int i = i0 + u * NT;
+            const u64 kk = ((u64)bias(v[u]) << 32) | (unsigned)(0xFFFFFFFFu - (unsigned)i);
+            ka = (i <= n1 && kk > ka) ? kk : ka;
+          }
+        }
       }
     }
     if (!folded && (mode == BGK_OVERLAP || mode == BGK_SEMIGLOBAL)) {
-#pragma unroll 4
-      for (int j = tid; j <= n2; j += NT) {          // last row, last max (:308, :369)
-        const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
-        kb = kk > kb ? kk : kb;
+      // last row, last max (:308, :369): the border cell (j = 0) apart, kEndU loads in flight
+      if (tid == 0) kb = (u64)bias(lastrowM(f, 0)) << 32;
+      if (n1 == 0) {
+        for (int j = 1 + tid; j <= n2; j += NT) {
+          const u64 kk = ((u64)bias(lastrowM(f, j)) << 32) | (unsigned)j;
+          kb = kk > kb ? kk : kb;
+        }
+      } else {
+        for (int j0 = 1 + tid; j0 <= n2; j0 += NT * kEndU) {
+          int v[kEndU];
+#pragma unroll
+          for (int u = 0; u < kEndU; ++u) v[u] = j0 + u * NT <= n2 ? f.lastrowMa[j0 + u * NT] : 0;
+#pragma unroll
+          for (int u = 0; u < kEndU; ++u) {
+            const int j = j0 + u * NT;
+            const u64 kk = ((u64)bias(lastrow_from(f, v[u], j)) << 32) | (unsigned)j;
+            kb = (j <= n2 && kk > kb) ? kk : kb;
+          }
+        }
       }
     }
     ka = wave_max_u64(ka);

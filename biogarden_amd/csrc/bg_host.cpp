@@ -1570,10 +1570,11 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.splitMap = h->splitMapBuf.as<int2>();
     if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;
     if (std::getenv("BG_FIN_SELFSERVE")) F.flags |= BG_FIN_SELFSERVE;
-    // the walker's priority 3 costs a many-pair batch's DP (the metric: 10 390 -> 10 530 GCUPS
-    // without it, tools/r04/prio_ab.sh); a WIDE batch's walks are its latency (BG_FIN_PRIO=1 /
-    // BG_FIN_NOPRIO=1 force either)
-    if (std::getenv("BG_FIN_NOPRIO") || (!h->wide && !std::getenv("BG_FIN_PRIO"))) F.flags |= BG_FIN_NOPRIO;
+    // the walker's priority 3 costs a many-pair linear batch's DP (the metric: 10 390 -> 10 530
+    // GCUPS without it, tools/r04/prio_ab.sh); a WIDE batch's walks are its latency, and the
+    // affine walks (recomputing with barriers) gain from it: MA 4 587 -> 4 714 GCUPS, C5 +0.9 %,
+    // C2 even (tools/r05/prio_ab.sh).  BG_FIN_PRIO=1 / BG_FIN_NOPRIO=1 force either.
+    if (std::getenv("BG_FIN_NOPRIO") || (!h->wide && !h->ack && !std::getenv("BG_FIN_PRIO"))) F.flags |= BG_FIN_NOPRIO;
     if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(128 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 128 * np, fs));
