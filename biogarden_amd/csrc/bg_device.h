@@ -249,6 +249,11 @@ struct BgFinishArgs {
   int32_t segc;
   int32_t* split;
   const int2* splitMap;
+  // linear checkpoint traceback's helpers: chunks prefetched left of the walker in its strip
+  // (0 .. kSpecDepth) and the rows from the strip's top within which the strip above is
+  // prefetched (bg_host.cpp: BG_SPEC="depth,rows")
+  int32_t specDepth;
+  int32_t specAbove;
 };
 
 // BgFinishArgs::phase

@@ -177,9 +177,10 @@ template <int R>
 __host__ __device__ constexpr int ack_prof_ints(int K) { return K * 64 * AffW<R>::v; }
 // chunk map: direct-mapped (strip & 15, chunk & 15) -> (s << 20 | c << 4 | slot)
 constexpr int kCkMapEntries = 256;
-// asynchronous recomputation: prefetch the strip above once the walker is this close to it
-constexpr int kAboveRows = 128;
-// ... and this many chunks ahead of the walker in its strip / in the strip above
+// asynchronous recomputation: at most this many chunks ahead of the walker in its strip / in the
+// strip above (the depth used, and how close to the strip's top the strip above is prefetched,
+// are BgFinishArgs::specDepth / specAbove: tools/r05/spec_ab.sh measured less speculation only
+// adding misses — every recomputed chunk is one the walk needs)
 #ifndef BG_SPEC_DEPTH
 #define BG_SPEC_DEPTH 2
 #endif
@@ -813,8 +814,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         // up to kSpecDepth chunks left of the walker in its strip, down to the predicted exit;
         // the strip above only near its boundary (earlier, the entry column is a poor guess)
         for (int d = 1; d <= kSpecDepth; ++d) {
-          cand[1 + d] = ccw - d >= cExit ? mk(sw, ccw - d) : -1;
-          cand[1 + kSpecDepth + d] = remw < kAboveRows ? mk(sw - 1, xE + 1 - d) : -1;
+          cand[1 + d] = (d <= F.specDepth && ccw - d >= cExit) ? mk(sw, ccw - d) : -1;
+          cand[1 + kSpecDepth + d] = (d <= F.specDepth && remw < F.specAbove) ? mk(sw - 1, xE + 1 - d) : -1;
         }
         auto dead = [&](int kk) { const int ss = kk >> 16, cc = kk & 0xffff; return ss > sw || (ss == sw && cc > ccw); };
         auto guarded = [&](int kk) {

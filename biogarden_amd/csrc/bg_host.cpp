@@ -1566,6 +1566,15 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.flags = h->finFlags;
     F.phase = BG_PH_FULL;
     F.segc = h->segc;
+    {
+      static const int2 spec = [] {
+        int d = 2, r = 128;
+        if (const char* e = std::getenv("BG_SPEC")) std::sscanf(e, "%d,%d", &d, &r);
+        return make_int2(std::min(std::max(d, 0), 2), std::max(r, 0));
+      }();
+      F.specDepth = spec.x;
+      F.specAbove = spec.y;
+    }
     F.split = S.split.as<int32_t>();
     F.splitMap = h->splitMapBuf.as<int2>();
     if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;

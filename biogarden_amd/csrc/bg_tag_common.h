@@ -20,6 +20,7 @@ struct TagStrip {
 
 struct TagCtx {
   int a, b, mode, n1, n2, rowbase, orow, lane;
+  bool repeatN1 = false;    // score_chunk: rows below n1 take row n1's value at column 0
   uint32_t* trace;          // this strip's trace
   int32_t* bndOut;          // this strip's boundary row (X forms), 64-column blocks
   int32_t* lastcol;         // M(i, n2)
@@ -261,7 +262,8 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
 #pragma unroll
           for (int k = 0; k < R; ++k) {
             const int i = C.rowbase + k + 1;
-            S.Y[k] = rst ? wadd(col0_M(C.mode, i, a, C.b), -wmul(a, i)) : S.Y[k];
+            const int ii = (C.repeatN1 && i > C.n1) ? C.n1 : i;       // rows below n1: row n1's
+            S.Y[k] = rst ? wadd(col0_M(C.mode, ii, a, C.b), -wmul(a, ii)) : S.Y[k];
           }
           S.Xlast = rst ? S.Y[R - 1] : S.Xlast;
         }

@@ -241,6 +241,14 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
     const int lastRow = n1 - 1 - s * ROWS;
     const int olane = lastStrip ? lastRow / R : BG_WAVE - 1;
     C.orow = lastStrip ? lastRow % R : R - 1;
+    // score-only strips (not WIDE): the rows below row n1 of the last strip are made to repeat row
+    // n1 — profile bytes -128 and row n1's column-0 value there, so max3 always takes the row above
+    // (M'(i, j) >= M'(i, j - 1) in the frame) — and the lane holding row n1 hands it down as its
+    // last row: the last strip runs the plain step instead of a select per row and step (1.8 % of
+    // the metric DP's VALU).  Nothing reads those rows: the traceback never walks below row n1.
+    const bool repeatN1 = CKPT && !WIDE && lastStrip && C.orow != R - 1;
+    if (repeatN1) C.orow = R - 1;
+    C.repeatN1 = repeatN1;
     const bool selRow = C.orow != R - 1;
     C.oLane = (lane <= olane ? C.ring : dummyRing) + 64 - lane;
     C.trace = A.trace + P.trace_off / 4 + (size_t)s * stripDw;
@@ -261,8 +269,9 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
       const int i = C.rowbase + k + 1;
       const int q = (i <= n1) ? qk[k] : 0;
       if constexpr (CKPT) {
-        pk[k] = A.profile[192 + (q >> 3)];                // 4 codes x int8 S - 2a
-        S.Y[k] = wadd(col0_M(mode, i, a, b), -wmul(a, i));
+        pk[k] = (repeatN1 && i > n1) ? (int)0x80808080 : A.profile[192 + (q >> 3)];   // 4 codes x int8 S - 2a
+        const int ii = (repeatN1 && i > n1) ? n1 : i;
+        S.Y[k] = wadd(col0_M(mode, ii, a, b), -wmul(a, ii));
       } else {
         pk[k] = A.profile[(k == 0 ? 64 : 128) + (q >> 3)];   // 4 codes x int8
         S.Y[k] = col0_Y(mode, i, a, b);
