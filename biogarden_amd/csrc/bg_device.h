@@ -35,6 +35,9 @@ struct BgPair {
   int32_t buf_cols;
   uint64_t ops_off;    // byte offset of this pair's packed core ops (ceil((n1+n2)/4) bytes)
   uint64_t split_off;  // split traceback (bg_split.hip): int32 offset of the pair's split area
+  int32_t lane0;       // grouped pairs (bg_grp_kernel.hip): the pair's first lane in its wave's
+                       // checkpoints (16 g); 0 otherwise
+  int32_t lanes;       // lanes per strip: 64, or 16 for grouped pairs
 };
 
 // ---- split traceback (WIDE linear checkpoint batches).  The walk of one long
@@ -208,6 +211,9 @@ struct BgDpArgs {
   int32_t* split;
   int32_t segc;
   uint32_t* resident;
+  // grouped single-strip pairs (bg_grp_kernel.hip): per wave four plan indices (-1: padding)
+  const int32_t* grp;
+  int32_t ngroups;
 };
 
 struct BgFinishArgs {
@@ -254,6 +260,9 @@ struct BgFinishArgs {
   // prefetched (bg_host.cpp: BG_SPEC="depth,rows")
   int32_t specDepth;
   int32_t specAbove;
+  // grouped single-strip pairs (bg_grp_kernel.hip): chunks are recomputed as 16-lane jobs, up to
+  // four per pass, into 16-lane slots
+  int32_t grouped;
 };
 
 // BgFinishArgs::phase

@@ -104,6 +104,85 @@ __host__ __device__ constexpr int ck_slot_dw() { return 2 * R * BG_WAVE * 2; }
 template <int R>
 __host__ __device__ constexpr int ck_wave_ints() { return 64 + 4 * 64 * ProfW<R>::v + 96; }
 
+// Grouped pairs (BgFinishArgs::grouped, bg_grp_kernel.hip): the pair holds 16 lanes of its wave's
+// checkpoints (from BgPair::lane0), a slot holds one chunk as [half][row k][16 lanes] x uint2, and
+// one pass recomputes up to four chunks of the pair, one per 16-lane DPP row.  Per wave: four
+// staged top blocks (row 0), the lanes' profile entries and four 192-code stages.
+template <int R>
+__host__ __device__ constexpr int ck_grp_slot_dw() { return 2 * R * 16 * 2; }
+template <int R>
+__host__ __device__ constexpr int ck_grp_wave_ints() { return 4 * 64 + 4 * 64 * ProfW<R>::v + 4 * 96; }
+constexpr int kGrpSlots = 8;
+
+template <int R>
+__device__ void recompute_grp(const BgFinishArgs& F, const BgPair& P, int nj, const int (&chunks)[4],
+                              const int (&zs)[4], uint32_t* win, int* area, int lane) {
+  constexpr int RW = ProfW<R>::v;
+  const int n1 = P.n1, n2 = P.n2, NC = P.nc;
+  const int a = F.open, b = F.ext, mode = F.mode;
+  const int j = lane >> 4, ql = lane & 15;
+  const int jj = j < nj ? j : 0;
+  const int c = jj == 0 ? chunks[0] : (jj == 1 ? chunks[1] : (jj == 2 ? chunks[2] : chunks[3]));
+  const int z = jj == 0 ? zs[0] : (jj == 1 ? zs[1] : (jj == 2 ? zs[2] : zs[3]));
+  int* bIn = area + j * 64;
+  int* profTab = area + 4 * 64;
+  uint16_t* stage = reinterpret_cast<uint16_t*>(profTab + 4 * 64 * RW) + j * 192;
+  TagCtx C;
+  TagStrip<R> S;
+  C.a = a; C.b = b; C.mode = mode; C.n1 = n1; C.n2 = n2; C.lane = ql;
+  C.rowbase = ql * R;
+  C.orow = R - 1;
+  C.lastcol = nullptr; C.ring = nullptr; C.oLane = nullptr; C.mail = nullptr; C.bndOut = nullptr;
+  const uint8_t* c1 = F.codes1 + P.off1;
+  const uint8_t* g2 = F.codes2 + P.off2;
+  int pk[R];
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = C.rowbase + k + 1;
+    const int qq = (i <= n1) ? c1[i - 1] : 0;
+    pk[k] = F.profile[(k == 0 ? 64 : 128) + (qq >> 3)];
+  }
+#pragma unroll
+  for (int cd = 0; cd < 4; ++cd)
+#pragma unroll
+    for (int wd = 0; wd < RW; ++wd) {
+      unsigned v = 0;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb)
+        if (wd * 4 + bb < R) v |= (((unsigned)pk[wd * 4 + bb] >> (8 * cd)) & 0xffu) << (8 * bb);
+      profTab[(cd * 64 + lane) * RW + wd] = (int)v;
+    }
+  // the job's codes of columns c * 64 - 64 .. c * 64 + 127, 12 per job lane
+#pragma unroll
+  for (int m = 0; m < 12; ++m) {
+    const int xx = ql + 16 * m;
+    const int x = c * BG_CHUNK - 64 + xx;
+    const int v = g2[x < 0 ? 0 : (x >= n2 ? n2 - 1 : x)];
+    stage[xx] = (uint16_t)(((unsigned)x < (unsigned)n2) ? v * (32 * RW) : 0);
+  }
+  // row 0 above the pair's first lane at step u: column c * 64 + u (X form)
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int u = ql + 16 * m;
+    const int col = c * BG_CHUNK + u;
+    bIn[u] = 4 * wadd(row0_M(mode, col, a, b), -wmul(a, col)) + 2;
+  }
+  (void)NC;
+  const int32_t* ck = reinterpret_cast<const int32_t*>(F.trace + P.trace_off / 4) +
+                      (size_t)c * (R + 1) * BG_WAVE + P.lane0 + ql;
+#pragma unroll
+  for (int k = 0; k < R; ++k) { S.Y[k] = 4 * ck[k * BG_WAVE] + 3; S.tA[k] = 0; S.tB[k] = 0; }
+  S.topPrev = 4 * ck[R * BG_WAVE] + 2;
+  S.Xlast = S.Y[R - 1] - 1;
+  C.bIn = bIn;
+  C.profLane = reinterpret_cast<const uint8_t*>(profTab + lane * RW);
+  C.codeLane = stage + 63 - ql;
+  uint32_t* slot = win + (size_t)z * ck_grp_slot_dw<R>();
+  const bool edge = ballot(c == 0) != 0;
+  if (edge) tag_chunk_jobs<R, true>(S, C, c, slot, ql, j < nj);
+  else tag_chunk_jobs<R, false>(S, C, c, slot, ql, j < nj);
+}
+
 template <int R>
 __device__ void recompute_chunk(const BgFinishArgs& F, const BgPair& P, int s, int c,
                                 uint32_t* slot, int* area, int lane) {
@@ -279,11 +358,14 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   int* ckArea = sh + 64;
   constexpr bool ACK = CK && AFFINE;                  // affine / local checkpoint traceback
   constexpr bool LIN_CK = CK && !AFFINE;              // linear checkpoint traceback
-  const int ckAreaInts = ACK ? kAckWaveInts : ck_wave_ints<R>();
+  // grouped pairs (BgFinishArgs::grouped): 16-lane chunks, recomputed up to four per pass
+  const bool grpMode = LIN_CK && F.grouped;
+  const int ckAreaInts = ACK ? kAckWaveInts : (grpMode ? ck_grp_wave_ints<R>() : ck_wave_ints<R>());
   int* profShared = ckArea;                           // ACK: the strip's profile entries
   if constexpr (ACK) ckArea += F.area_ints;
   int profS = -1;                                     // ACK: strip whose profile is built
   constexpr int kSlotDw = ACK ? ack_slot_dw<R, MODE == BGK_LOCAL>() : ck_slot_dw<R>();
+  const int slotDw = grpMode ? ck_grp_slot_dw<R>() : kSlotDw;       // linear checkpoint slots
   const int NWV = (int)(blockDim.x >> 6);              // waves: walker + recompute helpers
   int* jscr = ckArea + (CK ? NWV * ckAreaInts : 0);
   // checkpoint mode: direct-mapped table (strip & 31, chunk & 31) -> (s << 20 | c << 4 | slot)
@@ -515,10 +597,12 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     for (int c = 0; c < 16; ++c) v |= (u64)((c & 8) ? 0 : ((3u << 2) | 2)) << (4 * c);
     return v;
   }();
-  constexpr int kCkSlots = ACK ? ack_slots<R>() : ck_slots<R>();
+  constexpr int kCkSlots0 = ACK ? ack_slots<R>() : ck_slots<R>();
+  constexpr int kCkSlots = (!ACK && kGrpSlots > kCkSlots0) ? kGrpSlots : kCkSlots0;
   int ckS[kCkSlots], ckC[kCkSlots];                  // checkpoint mode: resident chunks
   // slots in use (the host trades cache for more resident workgroups on many-pair batches)
-  const int nSlots = (F.nslots > 0 && F.nslots < kCkSlots) ? F.nslots : kCkSlots;
+  const int maxSlots = grpMode ? kGrpSlots : kCkSlots0;
+  const int nSlots = (F.nslots > 0 && F.nslots < maxSlots) ? F.nslots : maxSlots;
   int ckNext = 0;                                    // next slot to fill (FIFO)
 #pragma unroll
   for (int z = 0; z < kCkSlots; ++z) { ckS[z] = -1; ckC[z] = -1; }
@@ -555,7 +639,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         if constexpr (MODE == BGK_LOCAL) mt = ((wp[4 * R * BG_WAVE] >> bit) & 1) ? 3 : mt;
         return mt | ((xI ^ 1) << 2) | ((yI ^ 1) << 3);
       }
-      const uint32_t* wp = win + (size_t)z * kSlotDw + (((bl & 1) * R + q) * BG_WAVE + r) * 2;
+      const uint32_t* wp = grpMode ? win + (size_t)z * slotDw + (((bl & 1) * R + q) * 16 + r) * 2
+                                   : win + (size_t)z * kSlotDw + (((bl & 1) * R + q) * BG_WAVE + r) * 2;
       const uint2 v = *reinterpret_cast<const uint2*>(wp);
       const int u = t & 31;
       const int tg = (int)((u < 16 ? v.x : v.y) >> (2 * (u & 15))) & 3;
@@ -768,7 +853,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   // down to the predicted exit, then the predicted entry of the strip above.  Eviction: a chunk
   // right of or below the walker is dead (the walk only moves up / left); a request may also
   // evict any slot outside the walker's 2 x 2 chunk footprint (it is waiting, so it reads none).
-  const bool async = LIN_CK && NWV >= 2 && nSlots >= 5 && !(F.flags & BG_FIN_SYNC);
+  const bool async = LIN_CK && NWV >= 2 && nSlots >= 5 && !(F.flags & BG_FIN_SYNC) && !grpMode;
   asyncPos = async;
   if (async) {
     if (tid == 0) {
@@ -1205,7 +1290,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       // recompute the requested chunk and up to three chunks to its left (the walk heads up and
       // left), one per wave, into the oldest slots
       int list[4], nl = 0;
-      for (int d = 0; d < NWV && d < 4; ++d) {
+      for (int d = 0; d < (grpMode ? 4 : NWV) && d < 4; ++d) {
         const int cc = reqB0 - d;
         if (cc < 0) break;
         bool res = false;
@@ -1230,9 +1315,19 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             recompute_chunk_aff<R, MODE == BGK_LOCAL, false>(F, P, reqS, list[wid], slotp, areap, profShared,
                                                              lane, 0, 0, 0, nullptr);
         }
-        else
+        else if (!grpMode)
           recompute_chunk<R>(F, P, reqS, list[wid], win + (size_t)myz * kSlotDw,
                              ckArea + wid * ckAreaInts, lane);
+      }
+      if (!ACK && grpMode && wid == 0) {
+        // one wave, up to four 16-lane jobs: the requested chunk and those to its left
+        int chs[4], zq[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          chs[x] = x < nl ? list[x] : list[0];
+          zq[x] = (ckNext + (x < nl ? x : 0)) % nSlots;
+        }
+        if constexpr (!ACK) recompute_grp<R>(F, P, nl, chs, zq, win, ckArea, lane);
       }
       for (int x = 0; x < nl; ++x) {
         const int z = (ckNext + x) % nSlots;

@@ -10,6 +10,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <condition_variable>
 #include <cstdint>
@@ -17,10 +18,12 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <numeric>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "bg_device.h"
@@ -41,6 +44,9 @@ extern "C" int bg_endkey_blocks(void);
 extern "C" int bg_exit_lds_bytes(int R);
 extern "C" int bg_exit_conc_lds_bytes(int R);
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
+extern "C" size_t bg_finish_grp_lds_bytes(int R, int nslots, int nw, int* win_bytes);
+extern "C" void* bg_dp_grp_kernel_ptr(int R);
+extern "C" int bg_dp_grp_wave_lds_bytes(int R);
 extern "C" int bg_dp_tag_wave_lds_bytes(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes(int win_bytes);
@@ -248,6 +254,11 @@ struct bg_aligner {
   int codesInLds = 0;
   int auxLdsOff = 0;
   int wide = 0;                    // tagged kernel: pairs spread over groups of workgroups
+  // grouped DP (bg_grp_kernel.hip): short reads sharing a reference, four per wave; grpHost holds
+  // four plan indices per group (-1: an empty row)
+  int grouped = 0, ngroups = 0;
+  std::vector<int32_t> grpHost;
+  DevBuf grpBuf;
   // split traceback (bg_split.hip): WIDE linear checkpoint batches walk their pairs
   // strip by strip in parallel; BG_SPLIT=0 walks them whole (one workgroup per pair)
   int split = 0, segc = BG_SPLIT_SEGC, splitMargin = 0, splitClamp = 0, splitGrow = 0;
@@ -519,6 +530,67 @@ static int pipeline_phases(int S, int gw, int NC, int lag = 2) {
 // chunks after the one above (two for the anti-diagonal skew and the block, the rest hand-off),
 // and every caught-up consumer adds its hand-off latency to the pace of the strips below it.
 // Fitted on C3's DP at R = 2 / 4 / 5 / 8 (12.3 / 10.1 / 9.8 / 10.3 ms): R = 5.
+// Grouped planner (bg_grp_kernel.hip): every computed pair's read at most 160
+// rows and its reference shared by others (the same caller buffer, or equal bytes), so that four
+// pairs of one reference fill a wave's four 16-lane rows; R is the least with 16 R >= the longest
+// read.  Off when the groups would average under 2.5 pairs (BG_GROUPED=0 never, =1 at any fill).
+static bool plan_grouped(bg_aligner* h, size_t npairs, const size_t* n1, const size_t* n2,
+                         const uint8_t* const* s2, int* Rout, int* Wout, std::vector<int>& refOf) {
+  const char* e = std::getenv("BG_GROUPED");
+  if (e && e[0] == '0') return false;
+  const bool force = e && e[0] == '1';
+  size_t maxn1 = 0, ndp = 0;
+  for (size_t p = 0; p < npairs; ++p) {
+    if (h->prestatus[p] >= 0 || n1[p] == 0 || n2[p] == 0) continue;
+    if (n1[p] > 160) return false;
+    maxn1 = std::max(maxn1, n1[p]);
+    ++ndp;
+  }
+  if (ndp == 0 || (ndp < 64 && !force)) return false;
+  refOf.assign(npairs, -1);
+  std::map<std::pair<const uint8_t*, size_t>, int> byPtr;
+  std::unordered_map<uint64_t, std::vector<int>> bySig;
+  std::vector<size_t> repOf, count;
+  for (size_t p = 0; p < npairs; ++p) {
+    if (h->prestatus[p] >= 0 || n1[p] == 0 || n2[p] == 0) continue;
+    const auto key = std::make_pair(s2[p], n2[p]);
+    auto it = byPtr.find(key);
+    int cls = -1;
+    if (it != byPtr.end()) {
+      cls = it->second;
+    } else {
+      // a sampled signature, then the bytes against the class representatives that share it
+      uint64_t sig = 1469598103934665603ULL ^ n2[p];
+      const size_t step = std::max<size_t>(1, n2[p] / 64);
+      for (size_t x = 0; x < n2[p]; x += step) sig = (sig ^ s2[p][x]) * 1099511628211ULL;
+      std::vector<int>& cand = bySig[sig];
+      for (int c : cand)
+        if (std::memcmp(s2[repOf[c]], s2[p], n2[p]) == 0) { cls = c; break; }
+      if (cls < 0) {
+        cls = (int)repOf.size();
+        repOf.push_back(p);
+        count.push_back(0);
+        cand.push_back(cls);
+      }
+      byPtr.emplace(key, cls);
+    }
+    refOf[p] = cls;
+    ++count[cls];
+  }
+  size_t groups = 0;
+  for (size_t c : count) groups += (c + 3) / 4;
+  if (!force && 2 * ndp < 5 * groups) return false;
+  int R = 10;
+  for (int r : {2, 3, 4, 5, 8, 10})
+    if (16 * (size_t)r >= maxn1) { R = r; break; }
+  int W = 4;
+  if (const char* ew = std::getenv("BG_GRP_W")) W = std::min(16, std::max(1, std::atoi(ew)));
+  *Rout = R;
+  *Wout = W;
+  h->tagRow = 0;
+  return true;
+}
+
 static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t npairs, int* Rout,
                       int* Wout) {
   std::vector<size_t> comp;
@@ -606,7 +678,14 @@ static void fin_geom(const bg_aligner* h, size_t np, int* nw, int* nslots) {
   if (h->ack && h->local && np > (size_t)h->cus * 2) { *nw = 1; *nslots = 2; }
   if (const char* e = std::getenv("BG_FIN_WAVES")) *nw = std::min(4, std::max(1, std::atoi(e)));
   if (const char* e = std::getenv("BG_FIN_SLOTS")) *nslots = std::max(0, std::atoi(e));
+  // grouped pairs: the walker recomputes up to four 16-lane chunks in one pass itself (one wave)
+  // into small slots (bg_finish.h recompute_grp)
+  if (h->grouped) { *nw = 1; *nslots = 6; }
+  if (const char* e = std::getenv("BG_FIN_WAVES")) *nw = std::min(4, std::max(1, std::atoi(e)));
+  if (const char* e = std::getenv("BG_FIN_SLOTS")) *nslots = std::max(0, std::atoi(e));
+  if (h->grouped) *nw = 1;
   if (*nslots && *nslots < *nw + 1) *nslots = *nw + 1;
+  if (h->grouped && *nslots && *nslots < 4) *nslots = 4;
 }
 
 // LDS of one finish workgroup (and the window / recompute-area sizes it launches with)
@@ -615,6 +694,7 @@ static size_t fin_lds(const bg_aligner* h, int R, size_t np, int* win, int* area
   int nw = 4, ns = 0;
   fin_geom(h, np, &nw, &ns);
   if (h->ack) return bg_finish_ack_lds_bytes(R, h->kdim, h->local, ns, nw, win, area);
+  if (h->ckpt && h->grouped) return bg_finish_grp_lds_bytes(R, ns, nw, win);
   if (h->ckpt) return bg_finish_ck_lds_bytes(R, ns, nw, win);
   *win = bg_finish_window_bytes(R, h->affine, np, h->cus);
   return bg_finish_lds_bytes(*win);
@@ -918,7 +998,10 @@ plan_again:
   // of workgroups per pair in the tagged kernel's WIDE mode)
   int R = 8, W = 1;
   h->wide = 0;
-  if (h->tag && plan_wide(h, n1, n2, npairs, &R, &W)) h->wide = 1;
+  h->grouped = 0;
+  std::vector<int> refOf;     // grouped DP: caller pair -> reference class (-1: not grouped)
+  if (h->tag && h->ckpt && !h->finFlags && plan_grouped(h, npairs, n1, n2, s2, &R, &W, refOf)) h->grouped = 1;
+  else if (h->tag && plan_wide(h, n1, n2, npairs, &R, &W)) h->wide = 1;
   else plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
   if ((h->ckpt || h->ack) && ncomp &&
       ((maxn1 + 64 * R - 1) / (64 * R) >= BG_CK_MAX_STRIPS || maxn2 / 64 + 2 >= BG_CK_MAX_CHUNKS)) {
@@ -927,7 +1010,15 @@ plan_again:
   }
   tm.mark(kPhPlan, "plan");
   size_t lds = 0;
-  if (h->tag) {
+  if (h->grouped) {
+    // grouped DP (bg_grp_kernel.hip): the shared dummy ring (512 B), then per wave the row-0
+    // block, four output rings, profile entries and the chunk's codes
+    h->progOff = 0;
+    h->codesOff = 0;
+    h->codesInLds = 0;
+    h->auxLdsOff = 512;
+    lds = 512 + (size_t)W * bg_dp_grp_wave_lds_bytes(R);
+  } else if (h->tag) {
     // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
     // boundary block, output ring, profile entries, the current chunk's codes and the mailbox
     h->progOff = 0;                  // counters + shared dummy ring: 640 B
@@ -1120,6 +1211,42 @@ plan_again:
       for (const auto& kv : keyed) h->splitBases.push_back(kv.second);
     }
   }
+  if (h->grouped) {
+    // groups of four plan pairs of one reference class (plan order within a class: longest
+    // first), the largest groups first; a group's pairs share one wave's checkpoints
+    std::vector<std::vector<int>> byRef;
+    for (size_t q = 0; q < h->plan.size(); ++q) {
+      const int rc = refOf[h->plan[q].caller];
+      if (rc < 0) continue;
+      if ((size_t)rc >= byRef.size()) byRef.resize(rc + 1);
+      byRef[rc].push_back((int)q);
+    }
+    std::vector<std::array<int32_t, 4>> groups;
+    for (const auto& v : byRef)
+      for (size_t x = 0; x < v.size(); x += 4) {
+        std::array<int32_t, 4> gq = {-1, -1, -1, -1};
+        for (size_t y = 0; y < 4 && x + y < v.size(); ++y) gq[y] = v[x + y];
+        groups.push_back(gq);
+      }
+    std::stable_sort(groups.begin(), groups.end(), [&](const std::array<int32_t, 4>& x, const std::array<int32_t, 4>& y) {
+      return (uint64_t)h->plan[x[0]].n1 * h->plan[x[0]].n2 > (uint64_t)h->plan[y[0]].n1 * h->plan[y[0]].n2;
+    });
+    tro = 0;
+    h->grpHost.clear();
+    for (const auto& gq : groups) {
+      const BgPair& P0 = h->plan[gq[0]];
+      for (int y = 0; y < 4; ++y) {
+        h->grpHost.push_back(gq[y]);
+        if (gq[y] < 0) continue;
+        BgPair& P = h->plan[gq[y]];
+        P.trace_off = tro;
+        P.lane0 = 16 * y;
+        P.lanes = 16;
+      }
+      tro += round_up((uint64_t)P0.nc * (R + 1) * BG_WAVE * 4, 256);
+    }
+    h->ngroups = (int)groups.size();
+  }
   h->traceBytes = tro;
   h->opsBytes = po;
   h->compactExec = -1;
@@ -1132,12 +1259,13 @@ plan_again:
       !h->codes2.ensure(o2 + 16) || !h->lut.ensure(256) ||
       !h->prof.ensure(std::max<size_t>(4096, (size_t)h->pstride * h->pstride * 4 + 64)) || !h->pairs.ensure(sizeof(BgPair) * (h->plan.size() + 1)) ||
       !h->wgmapBuf.ensure(sizeof(int2) * (h->wgmap.size() + 1)) ||
+      (h->grouped && !h->grpBuf.ensure(4 * (h->grpHost.size() + 4))) ||
       !h->gprogBuf.ensure(4 * ((size_t)h->progWords + 1)) ||
       (h->split && (!h->splitMapBuf.ensure(sizeof(int2) * (h->splitMap.size() + 1)) ||
                     !h->splitBaseBuf.ensure(4 * (h->splitBases.size() + 1)))) ||
       (h->pglob && !h->profScratch.ensure((h->plan.size() + 1) * (size_t)h->W * h->kdim * 64 * 4 * 4)))
     return BG_E_NOMEM;
-  h->gridWgs = h->wide ? (int)h->wgmap.size() : (int)h->plan.size();
+  h->gridWgs = h->wide ? (int)h->wgmap.size() : h->grouped ? (h->ngroups + W - 1) / W : (int)h->plan.size();
   for (int z = 0; z < h->depth; ++z) {
     Slot& S = h->slot[z];
     if (!S.trace.ensure(tro + 256) || !S.bndM.ensure(bo * 4 + 256) ||
@@ -1260,6 +1388,8 @@ plan_again:
                           hipMemcpyHostToDevice, us));
   BG_HIP(hipMemcpyAsync(h->pairs.p, h->plan.data(), sizeof(BgPair) * h->plan.size(),
                           hipMemcpyHostToDevice, us));
+  if (h->grouped)
+    BG_HIP(hipMemcpyAsync(h->grpBuf.p, h->grpHost.data(), 4 * h->grpHost.size(), hipMemcpyHostToDevice, us));
   if (h->split) {
     BG_HIP(hipMemcpyAsync(h->splitMapBuf.p, h->splitMap.data(), sizeof(int2) * h->splitMap.size(),
                           hipMemcpyHostToDevice, us));
@@ -1400,7 +1530,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[0], ds));
   if (np) {
-    void* fn = h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : dp_fn(h, h->R);
+    void* fn = h->grouped ? bg_dp_grp_kernel_ptr(h->R)
+             : h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : dp_fn(h, h->R);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
     A.pairs = h->pairs.as<BgPair>();
@@ -1448,6 +1579,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.ext = h->b;
     A.mode = h->mode;
     A.npairs = (int32_t)np;
+    A.grp = h->grouped ? h->grpBuf.as<int32_t>() : nullptr;
+    A.ngroups = h->grouped ? h->ngroups : 0;
     void* args[] = {&A};
     if (h->lds > 65536)
       BG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds));
@@ -1564,6 +1697,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.ops = S.ops.as<uint8_t>();
     F.area_ints = 0;
     F.flags = h->finFlags;
+    F.grouped = h->grouped;
     F.phase = BG_PH_FULL;
     F.segc = h->segc;
     {
@@ -1607,7 +1741,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
     } else if (h->ckpt) {
       int win = 0;
-      const size_t lds = bg_finish_ck_lds_bytes(h->R, fns, fnw, &win);
+      const size_t lds = h->grouped ? bg_finish_grp_lds_bytes(h->R, fns, fnw, &win)
+                                    : bg_finish_ck_lds_bytes(h->R, fns, fnw, &win);
       F.win_bytes = win;
       void* ffn = bg_finish_ck_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
@@ -1886,6 +2021,7 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->fin_waves = h->finWaves;
   o->fin_slots = h->finSlots;
   o->split = h->split;
+  o->grouped = h->grouped ? h->ngroups : 0;
   return BG_OK;
 }
 

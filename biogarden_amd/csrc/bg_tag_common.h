@@ -293,6 +293,76 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
   if constexpr (VAR == TV_EDGE) store_lastcol<R>(Lc, C, t0);
 }
 
+// v_mov_b32_dpp row_shr:1 — lane r receives lane r-1 within its 16-lane row; the first lane of
+// each row keeps `old` (band recomputation: four independent 16-lane jobs per wave).
+__device__ __forceinline__ int dpp_rowshr1(int old, int src) {
+  return __builtin_amdgcn_update_dpp(old, src, 0x111, 0xf, 0xf, false);
+}
+
+// 16-lane recomputation (traceback of grouped pairs, BgFinishArgs::grouped): the tagged step of
+// tag_chunk over up to four 16-lane jobs in one wave.  Job j = lane / 16 recomputes one chunk of a
+// pair (C.lane = its lane 0 .. 15) from its checkpoint; its first lane's row above comes from its
+// own staged block (C.bIn, per lane), the others' from the lane above by row_shr:1.
+// cl0: this lane's job chunk (EDGE: column 0 of chunk 0 is reset per lane); the trace goes to
+// `slot` as [half h][row k][job lane ql] x uint2 (16-lane stride), when `store`.
+template <int R, bool EDGE>
+__device__ __forceinline__ void tag_chunk_jobs(TagStrip<R>& S, const TagCtx& C, int cl0, uint32_t* slot, int ql,
+                                               bool store) {
+  const int a = C.a;
+  const int sl = C.lane;
+  constexpr int RW = ProfW<R>::v;
+  int nTop = C.bIn[0];
+  ProfV<RW> nP = load_prof<RW>(C.profLane + C.codeLane[0]);
+  int nCode = C.codeLane[1];
+  const uint16_t* cl = C.codeLane + 2;
+  const int* bi = C.bIn + 1;
+#pragma unroll 1
+  for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h, cl += BG_TRACE_BLK, bi += BG_TRACE_BLK) {
+#pragma unroll
+    for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
+      const int u = h * BG_TRACE_BLK + uu;
+      const int topIn = nTop;
+      const ProfV<RW> P = nP;
+      nP = load_prof<RW>(C.profLane + nCode);
+      nCode = cl[uu];
+      nTop = bi[uu];
+      const int topX = dpp_rowshr1(topIn, S.Xlast);           // X form of (row above, j)
+      int dIn = S.topPrev;
+      int xo = topX;
+#pragma unroll
+      for (int k = 0; k < R; ++k) {
+        const int yo = S.Y[k];
+        const int d = add_sbyte(dIn, P.w[k >> 2], k & 3);
+        const int best = imax(imax(d, xo), yo);
+        if (uu < 16) { S.tA[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tA[k], 2); asm volatile("" : "+v"(S.tA[k])); }
+        else { S.tB[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tB[k], 2); asm volatile("" : "+v"(S.tB[k])); }
+        const int yn = best | 3;
+        dIn = yo;
+        xo = yn - 1;
+        S.Y[k] = yn;
+      }
+      S.topPrev = topX;
+      S.Xlast = xo;
+      if constexpr (EDGE) {
+        const bool rst = (cl0 == 0) && (u == sl);             // column 0 (aligner.rs:98-104)
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int i = C.rowbase + k + 1;
+          S.Y[k] = rst ? col0_Y(C.mode, i, a, C.b) : S.Y[k];
+        }
+        S.Xlast = rst ? S.Y[R - 1] - 1 : S.Xlast;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (store) {
+      uint32_t* tb = slot + (size_t)h * (R * 2 * 16) + ql * 2;
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        *reinterpret_cast<uint2*>(tb + k * 2 * 16) = make_uint2(S.tA[k], S.tB[k]);
+    }
+  }
+}
+
 // v_mov_b32_dpp wave_shl:1 — lane r receives lane r+1; lane 63 keeps `old`.
 __device__ __forceinline__ int dpp_shl1(int old, int src) {
   return __builtin_amdgcn_update_dpp(old, src, 0x130, 0xf, 0xf, false);

@@ -172,6 +172,8 @@ typedef struct bg_stats {
   int32_t fin_waves;       /* finish workgroup: waves (walker + recomputing helpers) */
   int32_t fin_slots;       /* finish workgroup: recomputed-chunk slots in use (0: all) */
   int32_t split;           /* 1: the traceback is split at strip boundaries (few long pairs) */
+  int32_t grouped;         /* pair groups of the grouped DP (four short reads per wave sharing one
+                              reference), 0: one wave per pair */
 } bg_stats;
 
 int bg_get_stats(bg_aligner* h, bg_stats* out);
