@@ -214,10 +214,13 @@ struct BgDpArgs {
   // grouped single-strip pairs (bg_grp_kernel.hip): per wave four plan indices (-1: padding)
   const int32_t* grp;
   int32_t ngroups;
+  // semiglobal / overlap: each grouped pair's last-row end-cell key (BgFinishArgs::keys[2 p + 1])
+  unsigned long long* keys;
 };
 
 struct BgFinishArgs {
-  const unsigned long long* keys;   // split HEAD: bg_endkey_kernel's keys (BgSplitArgs::endKeys), or nullptr
+  const unsigned long long* keys;   // split HEAD: bg_endkey_kernel's keys (BgSplitArgs::endKeys);
+                                    // grouped: the last-row keys the DP folded; or nullptr
   const BgPair* pairs;
   const uint8_t* seq1;     // raw bytes (the aligned strings are built from them)
   const uint8_t* seq2;

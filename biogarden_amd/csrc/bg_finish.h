@@ -339,7 +339,9 @@ __device__ void recompute_chunk_aff(const BgFinishArgs& F, const BgPair& P, int 
   }
 }
 
-template <int R, bool AFFINE, int MODE, bool CK = false>
+// GRP: grouped pairs (BgFinishArgs::grouped; own instantiations, bg_grp_finish.hip, so the
+// other checkpoint kernels carry none of its registers)
+template <int R, bool AFFINE, int MODE, bool CK = false, bool GRP = false>
 __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u64 tK0 = __builtin_readcyclecounter();       // BG_FINISH_TIMING: the kernel's phases
@@ -359,7 +361,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   constexpr bool ACK = CK && AFFINE;                  // affine / local checkpoint traceback
   constexpr bool LIN_CK = CK && !AFFINE;              // linear checkpoint traceback
   // grouped pairs (BgFinishArgs::grouped): 16-lane chunks, recomputed up to four per pass
-  const bool grpMode = LIN_CK && F.grouped;
+  constexpr bool grpMode = LIN_CK && GRP;
   const int ckAreaInts = ACK ? kAckWaveInts : (grpMode ? ck_grp_wave_ints<R>() : ck_wave_ints<R>());
   int* profShared = ckArea;                           // ACK: the strip's profile entries
   if constexpr (ACK) ckArea += F.area_ints;
@@ -422,6 +424,14 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     // split HEAD: the keys of i, j >= 1 were folded by bg_endkey_kernel; the border cells here
     const bool folded = ph == BG_PH_HEAD && F.keys != nullptr && n1 > 0 && n2 > 0 && P.nstrips > 0 &&
                         (mode == BGK_SEMIGLOBAL || mode == BGK_OVERLAP || mode == BGK_FITTING);
+    // grouped pairs (semiglobal / overlap): the DP folded the last row's key (bg_grp_kernel.hip)
+    const bool rowFolded = GRP && !folded && F.keys != nullptr && n1 > 0 && n2 > 0 && P.nstrips > 0 &&
+                           (mode == BGK_SEMIGLOBAL || mode == BGK_OVERLAP);
+    if (rowFolded && tid == 0) {
+      const u64 kb0 = (u64)bias(lastrowM(f, 0)) << 32;
+      kb = F.keys[2 * (size_t)pidx + 1];
+      kb = kb0 > kb ? kb0 : kb;
+    }
     if (folded) {
       if (tid == 0) {
         ka = F.keys[2 * (size_t)pidx];
@@ -464,7 +474,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         }
       }
     }
-    if (!folded && (mode == BGK_OVERLAP || mode == BGK_SEMIGLOBAL)) {
+    if (!folded && !rowFolded && (mode == BGK_OVERLAP || mode == BGK_SEMIGLOBAL)) {
       // last row, last max (:308, :369): the border cell (j = 0) apart, kEndU loads in flight
       if (tid == 0) kb = (u64)bias(lastrowM(f, 0)) << 32;
       if (n1 == 0) {
@@ -598,7 +608,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     return v;
   }();
   constexpr int kCkSlots0 = ACK ? ack_slots<R>() : ck_slots<R>();
-  constexpr int kCkSlots = (!ACK && kGrpSlots > kCkSlots0) ? kGrpSlots : kCkSlots0;
+  constexpr int kCkSlots = (grpMode && kGrpSlots > kCkSlots0) ? kGrpSlots : kCkSlots0;
   int ckS[kCkSlots], ckC[kCkSlots];                  // checkpoint mode: resident chunks
   // slots in use (the host trades cache for more resident workgroups on many-pair batches)
   const int maxSlots = grpMode ? kGrpSlots : kCkSlots0;
@@ -1319,7 +1329,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           recompute_chunk<R>(F, P, reqS, list[wid], win + (size_t)myz * kSlotDw,
                              ckArea + wid * ckAreaInts, lane);
       }
-      if (!ACK && grpMode && wid == 0) {
+      if (grpMode && wid == 0) {
         // one wave, up to four 16-lane jobs: the requested chunk and those to its left
         int chs[4], zq[4];
 #pragma unroll
@@ -1327,7 +1337,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
           chs[x] = x < nl ? list[x] : list[0];
           zq[x] = (ckNext + (x < nl ? x : 0)) % nSlots;
         }
-        if constexpr (!ACK) recompute_grp<R>(F, P, nl, chs, zq, win, ckArea, lane);
+        if constexpr (grpMode) recompute_grp<R>(F, P, nl, chs, zq, win, ckArea, lane);
       }
       for (int x = 0; x < nl; ++x) {
         const int z = (ckNext + x) % nSlots;
@@ -1406,20 +1416,46 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
 
   // ---------------- semiglobal prefix (:416-428) and tail columns: one residue run against gaps
   // each (prefix: s1[0, kstop) or s2[0, lstop); tail: s1[ei, n1) or s2[ej, n2))
-  // (the residues of GB rounds are loaded before any of their stores: a load after a store to
-  // a buffer that may alias it waits for the load before the store, one round trip per column)
+  // 16-byte stores between byte heads and tails (C4: ~10 k columns per pair, which byte stores
+  // of 8 loads per round took ~20 latency-bound rounds for); the residues' 16 bytes come from five
+  // dword-aligned loads and v_alignbyte.  Loads of GB blocks go before their stores (a load after a
+  // store to a buffer that may alias it waits for the store).
   auto gap_run = [&](int dst, const uint8_t* src, int n) {
-    constexpr int GB = 8;
+    if (n <= 0) return;
     uint8_t* os = colcase ? ob + dst : ob2 + dst;      // the residues' side
     uint8_t* og = colcase ? ob2 + dst : ob + dst;      // the gaps' side
-    for (int x0 = tid; x0 < n; x0 += GB * NT) {
-      uint8_t v[GB];
-#pragma unroll
-      for (int u = 0; u < GB; ++u) v[u] = (x0 + u * NT < n) ? src[x0 + u * NT] : (uint8_t)0;
+    {
+      const int hg = min(n, (int)((16u - ((unsigned)(uintptr_t)og & 15u)) & 15u));
+      const int bg = (n - hg) >> 4;
+      if (tid < hg) og[tid] = (uint8_t)'-';
+      uint4* ov = reinterpret_cast<uint4*>(og + hg);
+      for (int b = tid; b < bg; b += NT) ov[b] = make_uint4(0x2d2d2d2du, 0x2d2d2d2du, 0x2d2d2d2du, 0x2d2d2d2du);
+      for (int x = hg + 16 * bg + tid; x < n; x += NT) og[x] = (uint8_t)'-';
+    }
+    const int hs = min(n, (int)((16u - ((unsigned)(uintptr_t)os & 15u)) & 15u));
+    const int bs = (n - hs) >> 4;
+    const uint8_t hv = tid < hs ? src[tid] : (uint8_t)0;
+    const uint8_t* s0 = src + hs;
+    const unsigned sh = (unsigned)(uintptr_t)s0 & 3u;
+    const uint32_t* sa = reinterpret_cast<const uint32_t*>(s0 - sh);   // reads <= 4 bytes past n
+    uint4* ov = reinterpret_cast<uint4*>(os + hs);
+    constexpr int GB = 4;
+    for (int b0 = tid; b0 < bs; b0 += GB * NT) {
+      uint32_t w[GB][5];
 #pragma unroll
       for (int u = 0; u < GB; ++u)
-        if (x0 + u * NT < n) { os[x0 + u * NT] = v[u]; og[x0 + u * NT] = (uint8_t)'-'; }
+#pragma unroll
+        for (int q = 0; q < 5; ++q) w[u][q] = (b0 + u * NT < bs) ? sa[4 * (b0 + u * NT) + q] : 0u;
+#pragma unroll
+      for (int u = 0; u < GB; ++u)
+        if (b0 + u * NT < bs)
+          ov[b0 + u * NT] = make_uint4(__builtin_amdgcn_alignbyte(w[u][1], w[u][0], sh),
+                                       __builtin_amdgcn_alignbyte(w[u][2], w[u][1], sh),
+                                       __builtin_amdgcn_alignbyte(w[u][3], w[u][2], sh),
+                                       __builtin_amdgcn_alignbyte(w[u][4], w[u][3], sh));
     }
+    if (tid < hs) os[tid] = hv;
+    for (int x = hs + 16 * bs + tid; x < n; x += NT) os[x] = src[x];
   };
   gap_run(base, colcase ? f.s1 : f.s2, npre);
   gap_run(cap - ntail, colcase ? f.s1 + ei : f.s2 + ej, ntail);

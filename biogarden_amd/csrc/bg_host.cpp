@@ -45,6 +45,7 @@ extern "C" int bg_exit_lds_bytes(int R);
 extern "C" int bg_exit_conc_lds_bytes(int R);
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
 extern "C" size_t bg_finish_grp_lds_bytes(int R, int nslots, int nw, int* win_bytes);
+extern "C" void* bg_finish_grp_kernel_ptr(int R, int mode);
 extern "C" void* bg_dp_grp_kernel_ptr(int R);
 extern "C" int bg_dp_grp_wave_lds_bytes(int R);
 extern "C" int bg_dp_tag_wave_lds_bytes(int R);
@@ -530,6 +531,13 @@ static int pipeline_phases(int S, int gw, int NC, int lag = 2) {
 // chunks after the one above (two for the anti-diagonal skew and the block, the rest hand-off),
 // and every caught-up consumer adds its hand-off latency to the pace of the strips below it.
 // Fitted on C3's DP at R = 2 / 4 / 5 / 8 (12.3 / 10.1 / 9.8 / 10.3 ms): R = 5.
+// grouped semiglobal / overlap batches: the DP folds each pair's last-row end-cell key, so the
+// traceback's one wave does not fold 10 k-column rows (BG_GRP_FOLD=0: the finish folds them)
+static bool grp_fold(const bg_aligner* h) {
+  static const bool off = [] { const char* e = std::getenv("BG_GRP_FOLD"); return e && e[0] == '0'; }();
+  return h->grouped && !off && (h->mode == BG_SEMIGLOBAL || h->mode == BG_OVERLAP);
+}
+
 // Grouped planner (bg_grp_kernel.hip): every computed pair's read at most 160
 // rows and its reference shared by others (the same caller buffer, or equal bytes), so that four
 // pairs of one reference fill a wave's four 16-lane rows; R is the least with 16 R >= the longest
@@ -683,7 +691,6 @@ static void fin_geom(const bg_aligner* h, size_t np, int* nw, int* nslots) {
   if (h->grouped) { *nw = 1; *nslots = 6; }
   if (const char* e = std::getenv("BG_FIN_WAVES")) *nw = std::min(4, std::max(1, std::atoi(e)));
   if (const char* e = std::getenv("BG_FIN_SLOTS")) *nslots = std::max(0, std::atoi(e));
-  if (h->grouped) *nw = 1;
   if (*nslots && *nslots < *nw + 1) *nslots = *nw + 1;
   if (h->grouped && *nslots && *nslots < 4) *nslots = 4;
 }
@@ -1272,7 +1279,7 @@ plan_again:
         !S.bndX.ensure((h->affine || h->ack) ? bo * 4 + 256 : 256) || !S.aux.ensure(ao * 4 + 256) ||
         !S.out1.ensure(oo + 16) || !S.out2.ensure(oo + 16) || !S.ops.ensure(po + 16) ||
         !S.results.ensure(sizeof(BgResult) * (h->plan.size() + 1)) ||
-        (h->split && !S.keys.ensure(16 * (h->plan.size() + 1))) ||
+        ((h->split || h->grouped) && !S.keys.ensure(16 * (h->plan.size() + 1))) ||
         (h->split && !S.xcnt.ensure(8 * ((size_t)h->plan.size() * h->splitXBlocks + 1))) ||
         (h->split && !S.split.ensure(h->splitInts * 4 + 256)) ||
         (h->wide && !S.gprog.ensure(4 * ((size_t)h->progWords + 8))))
@@ -1581,6 +1588,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.npairs = (int32_t)np;
     A.grp = h->grouped ? h->grpBuf.as<int32_t>() : nullptr;
     A.ngroups = h->grouped ? h->ngroups : 0;
+    // semiglobal / overlap: the grouped DP folds each pair's last-row end-cell key
+    A.keys = grp_fold(h) ? S.keys.as<unsigned long long>() : nullptr;
     void* args[] = {&A};
     if (h->lds > 65536)
       BG_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->lds));
@@ -1670,7 +1679,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   BG_HIP(hipEventRecord(e[2], fs));
   if (np) {
     BgFinishArgs F;
-    F.keys = nullptr;
+    F.keys = grp_fold(h) ? S.keys.as<unsigned long long>() : nullptr;
     F.pairs = h->pairs.as<BgPair>();
     F.seq1 = h->seq1.as<uint8_t>();
     F.seq2 = h->seq2.as<uint8_t>();
@@ -1744,7 +1753,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       const size_t lds = h->grouped ? bg_finish_grp_lds_bytes(h->R, fns, fnw, &win)
                                     : bg_finish_ck_lds_bytes(h->R, fns, fnw, &win);
       F.win_bytes = win;
-      void* ffn = bg_finish_ck_kernel_ptr(h->R, h->mode);
+      void* ffn = h->grouped ? bg_finish_grp_kernel_ptr(h->R, h->mode) : bg_finish_ck_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       if (!h->split) {
         BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));

@@ -691,22 +691,6 @@ extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_byt
   return (size_t)*win_bytes + 64 * 4 + (size_t)nw * area * 4 + kCkMapEntries * 4;  // + chunk map
 }
 
-// the same for grouped pairs (BgFinishArgs::grouped): kGrpSlots 16-lane chunk slots
-extern "C" size_t bg_finish_grp_lds_bytes(int R, int nslots, int nw, int* win_bytes) {
-  int slot = 0, area = 0;
-  switch (R) {
-    case 2: slot = ck_grp_slot_dw<2>(); area = ck_grp_wave_ints<2>(); break;
-    case 3: slot = ck_grp_slot_dw<3>(); area = ck_grp_wave_ints<3>(); break;
-    case 4: slot = ck_grp_slot_dw<4>(); area = ck_grp_wave_ints<4>(); break;
-    case 5: slot = ck_grp_slot_dw<5>(); area = ck_grp_wave_ints<5>(); break;
-    case 8: slot = ck_grp_slot_dw<8>(); area = ck_grp_wave_ints<8>(); break;
-    default: slot = ck_grp_slot_dw<10>(); area = ck_grp_wave_ints<10>(); break;
-  }
-  const int ns = (nslots > 0 && nslots < kGrpSlots) ? nslots : kGrpSlots;
-  *win_bytes = std::max(ns * slot * 4, 2 * 256 * 4);
-  return (size_t)*win_bytes + 64 * 4 + (size_t)nw * area * 4 + kCkMapEntries * 4;
-}
-
 template <int R, bool AF>
 static void* finish_ptr(int mode) {
   switch (mode) {
