@@ -69,7 +69,8 @@ class BgStats(ctypes.Structure):
                 ("checkpoint", ctypes.c_int32),
                 ("dp_ms", ctypes.c_float), ("finish_ms", ctypes.c_float),
                 ("fin_waves", ctypes.c_int32), ("fin_slots", ctypes.c_int32),
-                ("split", ctypes.c_int32), ("grouped", ctypes.c_int32)]
+                ("split", ctypes.c_int32), ("grouped", ctypes.c_int32),
+                ("group_pairs", ctypes.c_int32)]
 
 
 class BgFastaBatch(ctypes.Structure):

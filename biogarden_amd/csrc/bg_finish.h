@@ -104,23 +104,25 @@ __host__ __device__ constexpr int ck_slot_dw() { return 2 * R * BG_WAVE * 2; }
 template <int R>
 __host__ __device__ constexpr int ck_wave_ints() { return 64 + 4 * 64 * ProfW<R>::v + 96; }
 
-// Grouped pairs (BgFinishArgs::grouped, bg_grp_kernel.hip): the pair holds 16 lanes of its wave's
-// checkpoints (from BgPair::lane0), a slot holds one chunk as [half][row k][16 lanes] x uint2, and
-// one pass recomputes up to four chunks of the pair, one per 16-lane DPP row.  Per wave: four
-// staged top blocks (row 0), the lanes' profile entries and four 192-code stages.
-template <int R>
-__host__ __device__ constexpr int ck_grp_slot_dw() { return 2 * R * 16 * 2; }
+// Grouped pairs (BgFinishArgs::grouped, bg_grp_kernel.hip, P pairs per wave): the pair holds
+// L = 64 / P lanes of its wave's checkpoints (from BgPair::lane0), a slot holds one chunk as
+// [half][row k][L lanes] x uint2, and one pass recomputes up to P chunks of the pair, one per
+// L-lane job.  Per wave (sized for P = 4): four staged top blocks (row 0), the lanes' profile
+// entries and four 192-code stages.
+template <int R, int P>
+__host__ __device__ constexpr int ck_grp_slot_dw() { return 2 * R * (64 / P) * 2; }
 template <int R>
 __host__ __device__ constexpr int ck_grp_wave_ints() { return 4 * 64 + 4 * 64 * ProfW<R>::v + 4 * 96; }
 constexpr int kGrpSlots = 8;
 
-template <int R>
+template <int R, int GP>
 __device__ void recompute_grp(const BgFinishArgs& F, const BgPair& P, int nj, const int (&chunks)[4],
                               const int (&zs)[4], uint32_t* win, int* area, int lane) {
   constexpr int RW = ProfW<R>::v;
+  constexpr int L = 64 / GP;
   const int n1 = P.n1, n2 = P.n2, NC = P.nc;
   const int a = F.open, b = F.ext, mode = F.mode;
-  const int j = lane >> 4, ql = lane & 15;
+  const int j = lane / L, ql = lane % L;
   const int jj = j < nj ? j : 0;
   const int c = jj == 0 ? chunks[0] : (jj == 1 ? chunks[1] : (jj == 2 ? chunks[2] : chunks[3]));
   const int z = jj == 0 ? zs[0] : (jj == 1 ? zs[1] : (jj == 2 ? zs[2] : zs[3]));
@@ -152,18 +154,18 @@ __device__ void recompute_grp(const BgFinishArgs& F, const BgPair& P, int nj, co
         if (wd * 4 + bb < R) v |= (((unsigned)pk[wd * 4 + bb] >> (8 * cd)) & 0xffu) << (8 * bb);
       profTab[(cd * 64 + lane) * RW + wd] = (int)v;
     }
-  // the job's codes of columns c * 64 - 64 .. c * 64 + 127, 12 per job lane
+  // the job's codes of columns c * 64 - 64 .. c * 64 + 127, 192 / L per job lane
 #pragma unroll
-  for (int m = 0; m < 12; ++m) {
-    const int xx = ql + 16 * m;
+  for (int m = 0; m < 192 / L; ++m) {
+    const int xx = ql + L * m;
     const int x = c * BG_CHUNK - 64 + xx;
     const int v = g2[x < 0 ? 0 : (x >= n2 ? n2 - 1 : x)];
     stage[xx] = (uint16_t)(((unsigned)x < (unsigned)n2) ? v * (32 * RW) : 0);
   }
   // row 0 above the pair's first lane at step u: column c * 64 + u (X form)
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int u = ql + 16 * m;
+  for (int m = 0; m < 64 / L; ++m) {
+    const int u = ql + L * m;
     const int col = c * BG_CHUNK + u;
     bIn[u] = 4 * wadd(row0_M(mode, col, a, b), -wmul(a, col)) + 2;
   }
@@ -177,10 +179,10 @@ __device__ void recompute_grp(const BgFinishArgs& F, const BgPair& P, int nj, co
   C.bIn = bIn;
   C.profLane = reinterpret_cast<const uint8_t*>(profTab + lane * RW);
   C.codeLane = stage + 63 - ql;
-  uint32_t* slot = win + (size_t)z * ck_grp_slot_dw<R>();
+  uint32_t* slot = win + (size_t)z * ck_grp_slot_dw<R, GP>();
   const bool edge = ballot(c == 0) != 0;
-  if (edge) tag_chunk_jobs<R, true>(S, C, c, slot, ql, j < nj);
-  else tag_chunk_jobs<R, false>(S, C, c, slot, ql, j < nj);
+  if (edge) tag_chunk_jobs<R, true, GP>(S, C, c, slot, ql, j < nj);
+  else tag_chunk_jobs<R, false, GP>(S, C, c, slot, ql, j < nj);
 }
 
 template <int R>
@@ -339,9 +341,9 @@ __device__ void recompute_chunk_aff(const BgFinishArgs& F, const BgPair& P, int 
   }
 }
 
-// GRP: grouped pairs (BgFinishArgs::grouped; own instantiations, bg_grp_finish.hip, so the
-// other checkpoint kernels carry none of its registers)
-template <int R, bool AFFINE, int MODE, bool CK = false, bool GRP = false>
+// GRP: grouped pairs, GRP per wave (BgFinishArgs::grouped; own instantiations, bg_grp_finish.hip,
+// so the other checkpoint kernels carry none of its registers); 0 otherwise
+template <int R, bool AFFINE, int MODE, bool CK = false, int GRP = 0>
 __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const u64 tK0 = __builtin_readcyclecounter();       // BG_FINISH_TIMING: the kernel's phases
@@ -361,13 +363,14 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   constexpr bool ACK = CK && AFFINE;                  // affine / local checkpoint traceback
   constexpr bool LIN_CK = CK && !AFFINE;              // linear checkpoint traceback
   // grouped pairs (BgFinishArgs::grouped): 16-lane chunks, recomputed up to four per pass
-  constexpr bool grpMode = LIN_CK && GRP;
+  constexpr bool grpMode = LIN_CK && GRP > 0;
+  constexpr int GL = GRP > 0 ? 64 / GRP : 64;          // grouped: lanes per pair
   const int ckAreaInts = ACK ? kAckWaveInts : (grpMode ? ck_grp_wave_ints<R>() : ck_wave_ints<R>());
   int* profShared = ckArea;                           // ACK: the strip's profile entries
   if constexpr (ACK) ckArea += F.area_ints;
   int profS = -1;                                     // ACK: strip whose profile is built
   constexpr int kSlotDw = ACK ? ack_slot_dw<R, MODE == BGK_LOCAL>() : ck_slot_dw<R>();
-  const int slotDw = grpMode ? ck_grp_slot_dw<R>() : kSlotDw;       // linear checkpoint slots
+  const int slotDw = grpMode ? ck_grp_slot_dw<R, (GRP > 0 ? GRP : 4)>() : kSlotDw;   // linear checkpoint slots
   const int NWV = (int)(blockDim.x >> 6);              // waves: walker + recompute helpers
   int* jscr = ckArea + (CK ? NWV * ckAreaInts : 0);
   // checkpoint mode: direct-mapped table (strip & 31, chunk & 31) -> (s << 20 | c << 4 | slot)
@@ -425,7 +428,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     const bool folded = ph == BG_PH_HEAD && F.keys != nullptr && n1 > 0 && n2 > 0 && P.nstrips > 0 &&
                         (mode == BGK_SEMIGLOBAL || mode == BGK_OVERLAP || mode == BGK_FITTING);
     // grouped pairs (semiglobal / overlap): the DP folded the last row's key (bg_grp_kernel.hip)
-    const bool rowFolded = GRP && !folded && F.keys != nullptr && n1 > 0 && n2 > 0 && P.nstrips > 0 &&
+    const bool rowFolded = GRP > 0 && !folded && F.keys != nullptr && n1 > 0 && n2 > 0 && P.nstrips > 0 &&
                            (mode == BGK_SEMIGLOBAL || mode == BGK_OVERLAP);
     if (rowFolded && tid == 0) {
       const u64 kb0 = (u64)bias(lastrowM(f, 0)) << 32;
@@ -649,7 +652,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         if constexpr (MODE == BGK_LOCAL) mt = ((wp[4 * R * BG_WAVE] >> bit) & 1) ? 3 : mt;
         return mt | ((xI ^ 1) << 2) | ((yI ^ 1) << 3);
       }
-      const uint32_t* wp = grpMode ? win + (size_t)z * slotDw + (((bl & 1) * R + q) * 16 + r) * 2
+      const uint32_t* wp = grpMode ? win + (size_t)z * slotDw + (((bl & 1) * R + q) * GL + r) * 2
                                    : win + (size_t)z * kSlotDw + (((bl & 1) * R + q) * BG_WAVE + r) * 2;
       const uint2 v = *reinterpret_cast<const uint2*>(wp);
       const int u = t & 31;
@@ -1300,7 +1303,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
       // recompute the requested chunk and up to three chunks to its left (the walk heads up and
       // left), one per wave, into the oldest slots
       int list[4], nl = 0;
-      for (int d = 0; d < (grpMode ? 4 : NWV) && d < 4; ++d) {
+      for (int d = 0; d < (grpMode ? GRP : NWV) && d < 4; ++d) {
         const int cc = reqB0 - d;
         if (cc < 0) break;
         bool res = false;
@@ -1330,14 +1333,14 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                              ckArea + wid * ckAreaInts, lane);
       }
       if (grpMode && wid == 0) {
-        // one wave, up to four 16-lane jobs: the requested chunk and those to its left
+        // one wave, up to GRP jobs: the requested chunk and those to its left
         int chs[4], zq[4];
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
           chs[x] = x < nl ? list[x] : list[0];
           zq[x] = (ckNext + (x < nl ? x : 0)) % nSlots;
         }
-        if constexpr (grpMode) recompute_grp<R>(F, P, nl, chs, zq, win, ckArea, lane);
+        if constexpr (grpMode) recompute_grp<R, GRP>(F, P, nl, chs, zq, win, ckArea, lane);
       }
       for (int x = 0; x < nl; ++x) {
         const int z = (ckNext + x) % nSlots;

@@ -44,10 +44,19 @@ extern "C" int bg_endkey_blocks(void);
 extern "C" int bg_exit_lds_bytes(int R);
 extern "C" int bg_exit_conc_lds_bytes(int R);
 extern "C" size_t bg_finish_ck_lds_bytes(int R, int nslots, int nw, int* win_bytes);
-extern "C" size_t bg_finish_grp_lds_bytes(int R, int nslots, int nw, int* win_bytes);
-extern "C" void* bg_finish_grp_kernel_ptr(int R, int mode);
-extern "C" void* bg_dp_grp_kernel_ptr(int R);
-extern "C" int bg_dp_grp_wave_lds_bytes(int R);
+extern "C" size_t bg_finish_grp4_lds_bytes(int R, int nslots, int nw, int* win_bytes);
+extern "C" size_t bg_finish_grp2_lds_bytes(int R, int nslots, int nw, int* win_bytes);
+extern "C" void* bg_finish_grp4_kernel_ptr(int R, int mode);
+extern "C" void* bg_finish_grp2_kernel_ptr(int R, int mode);
+extern "C" void* bg_dp_grp_kernel_ptr(int R, int P);
+extern "C" int bg_dp_grp_wave_lds_bytes(int R, int P);
+// grouped pairs, P per wave (bg_grp_kernel.hip, bg_grp_finish.hip)
+static size_t bg_finish_grp_lds_bytes(int P, int R, int nslots, int nw, int* win) {
+  return P == 2 ? bg_finish_grp2_lds_bytes(R, nslots, nw, win) : bg_finish_grp4_lds_bytes(R, nslots, nw, win);
+}
+static void* bg_finish_grp_kernel_ptr(int P, int R, int mode) {
+  return P == 2 ? bg_finish_grp2_kernel_ptr(R, mode) : bg_finish_grp4_kernel_ptr(R, mode);
+}
 extern "C" int bg_dp_tag_wave_lds_bytes(int R);
 extern "C" void* bg_finish_kernel_ptr(int R, int affine, int mode);
 extern "C" size_t bg_finish_lds_bytes(int win_bytes);
@@ -255,8 +264,8 @@ struct bg_aligner {
   int codesInLds = 0;
   int auxLdsOff = 0;
   int wide = 0;                    // tagged kernel: pairs spread over groups of workgroups
-  // grouped DP (bg_grp_kernel.hip): short reads sharing a reference, four per wave; grpHost holds
-  // four plan indices per group (-1: an empty row)
+  // grouped DP (bg_grp_kernel.hip): short reads sharing a reference, `grouped` (P = 4 or 2) per
+  // wave, 0 off; grpHost holds P plan indices per group (-1: an empty row)
   int grouped = 0, ngroups = 0;
   std::vector<int32_t> grpHost;
   DevBuf grpBuf;
@@ -538,23 +547,28 @@ static bool grp_fold(const bg_aligner* h) {
   return h->grouped && !off && (h->mode == BG_SEMIGLOBAL || h->mode == BG_OVERLAP);
 }
 
-// Grouped planner (bg_grp_kernel.hip): every computed pair's read at most 160
-// rows and its reference shared by others (the same caller buffer, or equal bytes), so that four
-// pairs of one reference fill a wave's four 16-lane rows; R is the least with 16 R >= the longest
-// read.  Off when the groups would average under 2.5 pairs (BG_GROUPED=0 never, =1 at any fill).
-static bool plan_grouped(bg_aligner* h, size_t npairs, const size_t* n1, const size_t* n2,
-                         const uint8_t* const* s2, int* Rout, int* Wout, std::vector<int>& refOf) {
+// Grouped planner (bg_grp_kernel.hip): every computed pair's read at most 320
+// rows and its reference shared by others (the same caller buffer, or equal bytes), so that P
+// pairs of one reference fill a wave, 64 / P lanes each; R is the least with (64 / P) R >= the
+// longest read.  P = 4 (16-lane DPP rows) for reads up to 160, else P = 2 (a select per step).
+// P = 4 wins even at 2 waves per SIMD: C4's 8 192 pairs run their DP in 1.16 ms at P = 4 (R = 10,
+// 2 048 waves, 513 M VALU instructions) against 1.34 ms at P = 2 (R = 5, 4 096 waves, 674 M) —
+// the DP is VALU-bound (72 % of the SIMDs' quad-cycle issue), so fewer instructions per cell beat
+// more waves (profiles/r05/grouped/pmc_c4_p*.json).  Off when the groups would average under
+// 0.6 P pairs.  BG_GROUPED=0 never, =1 at any fill; BG_GRP_P=2 / 4 forces P.  Returns P, or 0.
+static int plan_grouped(bg_aligner* h, size_t npairs, const size_t* n1, const size_t* n2,
+                        const uint8_t* const* s2, int* Rout, int* Wout, std::vector<int>& refOf) {
   const char* e = std::getenv("BG_GROUPED");
-  if (e && e[0] == '0') return false;
+  if (e && e[0] == '0') return 0;
   const bool force = e && e[0] == '1';
   size_t maxn1 = 0, ndp = 0;
   for (size_t p = 0; p < npairs; ++p) {
     if (h->prestatus[p] >= 0 || n1[p] == 0 || n2[p] == 0) continue;
-    if (n1[p] > 160) return false;
+    if (n1[p] > 320) return 0;
     maxn1 = std::max(maxn1, n1[p]);
     ++ndp;
   }
-  if (ndp == 0 || (ndp < 64 && !force)) return false;
+  if (ndp == 0 || (ndp < 64 && !force)) return 0;
   refOf.assign(npairs, -1);
   std::map<std::pair<const uint8_t*, size_t>, int> byPtr;
   std::unordered_map<uint64_t, std::vector<int>> bySig;
@@ -585,18 +599,21 @@ static bool plan_grouped(bg_aligner* h, size_t npairs, const size_t* n1, const s
     refOf[p] = cls;
     ++count[cls];
   }
-  size_t groups = 0;
-  for (size_t c : count) groups += (c + 3) / 4;
-  if (!force && 2 * ndp < 5 * groups) return false;
+  size_t g4 = 0, g2 = 0;
+  for (size_t c : count) { g4 += (c + 3) / 4; g2 += (c + 1) / 2; }
+  int P = maxn1 <= 160 ? 4 : 2;
+  if (const char* ep = std::getenv("BG_GRP_P")) P = (ep[0] == '4' && maxn1 <= 160) ? 4 : 2;
+  const size_t groups = P == 4 ? g4 : g2;
+  if (!force && 10 * ndp < 6 * (size_t)P * groups) return 0;
   int R = 10;
   for (int r : {2, 3, 4, 5, 8, 10})
-    if (16 * (size_t)r >= maxn1) { R = r; break; }
+    if ((size_t)(64 / P) * r >= maxn1) { R = r; break; }
   int W = 4;
   if (const char* ew = std::getenv("BG_GRP_W")) W = std::min(16, std::max(1, std::atoi(ew)));
   *Rout = R;
   *Wout = W;
   h->tagRow = 0;
-  return true;
+  return P;
 }
 
 static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t npairs, int* Rout,
@@ -701,7 +718,7 @@ static size_t fin_lds(const bg_aligner* h, int R, size_t np, int* win, int* area
   int nw = 4, ns = 0;
   fin_geom(h, np, &nw, &ns);
   if (h->ack) return bg_finish_ack_lds_bytes(R, h->kdim, h->local, ns, nw, win, area);
-  if (h->ckpt && h->grouped) return bg_finish_grp_lds_bytes(R, ns, nw, win);
+  if (h->ckpt && h->grouped) return bg_finish_grp_lds_bytes(h->grouped, R, ns, nw, win);
   if (h->ckpt) return bg_finish_ck_lds_bytes(R, ns, nw, win);
   *win = bg_finish_window_bytes(R, h->affine, np, h->cus);
   return bg_finish_lds_bytes(*win);
@@ -1007,8 +1024,9 @@ plan_again:
   h->wide = 0;
   h->grouped = 0;
   std::vector<int> refOf;     // grouped DP: caller pair -> reference class (-1: not grouped)
-  if (h->tag && h->ckpt && !h->finFlags && plan_grouped(h, npairs, n1, n2, s2, &R, &W, refOf)) h->grouped = 1;
-  else if (h->tag && plan_wide(h, n1, n2, npairs, &R, &W)) h->wide = 1;
+  if (h->tag && h->ckpt && !h->finFlags) h->grouped = plan_grouped(h, npairs, n1, n2, s2, &R, &W, refOf);
+  if (h->grouped) {
+  } else if (h->tag && plan_wide(h, n1, n2, npairs, &R, &W)) h->wide = 1;
   else plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
   if ((h->ckpt || h->ack) && ncomp &&
       ((maxn1 + 64 * R - 1) / (64 * R) >= BG_CK_MAX_STRIPS || maxn2 / 64 + 2 >= BG_CK_MAX_CHUNKS)) {
@@ -1024,7 +1042,7 @@ plan_again:
     h->codesOff = 0;
     h->codesInLds = 0;
     h->auxLdsOff = 512;
-    lds = 512 + (size_t)W * bg_dp_grp_wave_lds_bytes(R);
+    lds = 512 + (size_t)W * bg_dp_grp_wave_lds_bytes(R, h->grouped);
   } else if (h->tag) {
     // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
     // boundary block, output ring, profile entries, the current chunk's codes and the mailbox
@@ -1219,8 +1237,9 @@ plan_again:
     }
   }
   if (h->grouped) {
-    // groups of four plan pairs of one reference class (plan order within a class: longest
-    // first), the largest groups first; a group's pairs share one wave's checkpoints
+    // groups of P plan pairs of one reference class (plan order within a class: longest first),
+    // the largest groups first; a group's pairs share one wave's checkpoints
+    const int GP = h->grouped;
     std::vector<std::vector<int>> byRef;
     for (size_t q = 0; q < h->plan.size(); ++q) {
       const int rc = refOf[h->plan[q].caller];
@@ -1230,9 +1249,9 @@ plan_again:
     }
     std::vector<std::array<int32_t, 4>> groups;
     for (const auto& v : byRef)
-      for (size_t x = 0; x < v.size(); x += 4) {
+      for (size_t x = 0; x < v.size(); x += GP) {
         std::array<int32_t, 4> gq = {-1, -1, -1, -1};
-        for (size_t y = 0; y < 4 && x + y < v.size(); ++y) gq[y] = v[x + y];
+        for (size_t y = 0; y < (size_t)GP && x + y < v.size(); ++y) gq[y] = v[x + y];
         groups.push_back(gq);
       }
     std::stable_sort(groups.begin(), groups.end(), [&](const std::array<int32_t, 4>& x, const std::array<int32_t, 4>& y) {
@@ -1242,13 +1261,13 @@ plan_again:
     h->grpHost.clear();
     for (const auto& gq : groups) {
       const BgPair& P0 = h->plan[gq[0]];
-      for (int y = 0; y < 4; ++y) {
+      for (int y = 0; y < GP; ++y) {
         h->grpHost.push_back(gq[y]);
         if (gq[y] < 0) continue;
         BgPair& P = h->plan[gq[y]];
         P.trace_off = tro;
-        P.lane0 = 16 * y;
-        P.lanes = 16;
+        P.lane0 = (64 / GP) * y;
+        P.lanes = 64 / GP;
       }
       tro += round_up((uint64_t)P0.nc * (R + 1) * BG_WAVE * 4, 256);
     }
@@ -1537,7 +1556,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[0], ds));
   if (np) {
-    void* fn = h->grouped ? bg_dp_grp_kernel_ptr(h->R)
+    void* fn = h->grouped ? bg_dp_grp_kernel_ptr(h->R, h->grouped)
              : h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : dp_fn(h, h->R);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
@@ -1750,10 +1769,10 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
     } else if (h->ckpt) {
       int win = 0;
-      const size_t lds = h->grouped ? bg_finish_grp_lds_bytes(h->R, fns, fnw, &win)
+      const size_t lds = h->grouped ? bg_finish_grp_lds_bytes(h->grouped, h->R, fns, fnw, &win)
                                     : bg_finish_ck_lds_bytes(h->R, fns, fnw, &win);
       F.win_bytes = win;
-      void* ffn = h->grouped ? bg_finish_grp_kernel_ptr(h->R, h->mode) : bg_finish_ck_kernel_ptr(h->R, h->mode);
+      void* ffn = h->grouped ? bg_finish_grp_kernel_ptr(h->grouped, h->R, h->mode) : bg_finish_ck_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       if (!h->split) {
         BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
@@ -2031,6 +2050,7 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->fin_slots = h->finSlots;
   o->split = h->split;
   o->grouped = h->grouped ? h->ngroups : 0;
+  o->group_pairs = h->grouped;
   return BG_OK;
 }
 

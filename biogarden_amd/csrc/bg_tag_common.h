@@ -299,15 +299,31 @@ __device__ __forceinline__ int dpp_rowshr1(int old, int src) {
   return __builtin_amdgcn_update_dpp(old, src, 0x111, 0xf, 0xf, false);
 }
 
-// 16-lane recomputation (traceback of grouped pairs, BgFinishArgs::grouped): the tagged step of
-// tag_chunk over up to four 16-lane jobs in one wave.  Job j = lane / 16 recomputes one chunk of a
-// pair (C.lane = its lane 0 .. 15) from its checkpoint; its first lane's row above comes from its
-// own staged block (C.bIn, per lane), the others' from the lane above by row_shr:1.
-// cl0: this lane's job chunk (EDGE: column 0 of chunk 0 is reset per lane); the trace goes to
-// `slot` as [half h][row k][job lane ql] x uint2 (16-lane stride), when `store`.
-template <int R, bool EDGE>
+// The row hand-off of P pairs per wave (64 / P lanes each, bg_grp_kernel.hip): lane r receives
+// lane r - 1 and a pair's first lane keeps `old` — row_shr:1 does both for P = 4; for P = 2,
+// wave_shr:1 and lane 32 takes `old` by a select.
+template <int P>
+__device__ __forceinline__ int grp_shr1(int old, int src, bool first) {
+  if constexpr (P == 4) {
+    (void)first;
+    return dpp_rowshr1(old, src);
+  } else {
+    const int v = dpp_shr1(old, src);
+    return first ? old : v;
+  }
+}
+
+// Recomputation for grouped pairs (BgFinishArgs::grouped): the tagged step of tag_chunk over up
+// to P jobs of 64 / P lanes in one wave.  Job j = lane / (64 / P) recomputes one chunk of a pair
+// (C.lane = its lane) from its checkpoint; its first lane's row above comes from its own staged
+// block (C.bIn, per lane), the others' from the lane above (grp_shr1).  cl0: this lane's job
+// chunk (EDGE: column 0 of chunk 0 is reset per lane); the trace goes to `slot` as [half h][row k]
+// [job lane ql] x uint2 (64 / P lane stride), when `store`.
+template <int R, bool EDGE, int P>
 __device__ __forceinline__ void tag_chunk_jobs(TagStrip<R>& S, const TagCtx& C, int cl0, uint32_t* slot, int ql,
                                                bool store) {
+  constexpr int L = 64 / P;
+  const bool first = C.lane == 0;
   const int a = C.a;
   const int sl = C.lane;
   constexpr int RW = ProfW<R>::v;
@@ -322,17 +338,17 @@ __device__ __forceinline__ void tag_chunk_jobs(TagStrip<R>& S, const TagCtx& C, 
     for (int uu = 0; uu < BG_TRACE_BLK; ++uu) {
       const int u = h * BG_TRACE_BLK + uu;
       const int topIn = nTop;
-      const ProfV<RW> P = nP;
+      const ProfV<RW> Pv = nP;
       nP = load_prof<RW>(C.profLane + nCode);
       nCode = cl[uu];
       nTop = bi[uu];
-      const int topX = dpp_rowshr1(topIn, S.Xlast);           // X form of (row above, j)
+      const int topX = grp_shr1<P>(topIn, S.Xlast, first);    // X form of (row above, j)
       int dIn = S.topPrev;
       int xo = topX;
 #pragma unroll
       for (int k = 0; k < R; ++k) {
         const int yo = S.Y[k];
-        const int d = add_sbyte(dIn, P.w[k >> 2], k & 3);
+        const int d = add_sbyte(dIn, Pv.w[k >> 2], k & 3);
         const int best = imax(imax(d, xo), yo);
         if (uu < 16) { S.tA[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tA[k], 2); asm volatile("" : "+v"(S.tA[k])); }
         else { S.tB[k] = __builtin_amdgcn_alignbit((unsigned)best, S.tB[k], 2); asm volatile("" : "+v"(S.tB[k])); }
@@ -355,10 +371,10 @@ __device__ __forceinline__ void tag_chunk_jobs(TagStrip<R>& S, const TagCtx& C, 
       __builtin_amdgcn_sched_barrier(0);
     }
     if (store) {
-      uint32_t* tb = slot + (size_t)h * (R * 2 * 16) + ql * 2;
+      uint32_t* tb = slot + (size_t)h * (R * 2 * L) + ql * 2;
 #pragma unroll
       for (int k = 0; k < R; ++k)
-        *reinterpret_cast<uint2*>(tb + k * 2 * 16) = make_uint2(S.tA[k], S.tB[k]);
+        *reinterpret_cast<uint2*>(tb + k * 2 * L) = make_uint2(S.tA[k], S.tB[k]);
     }
   }
 }

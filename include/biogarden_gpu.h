@@ -174,6 +174,7 @@ typedef struct bg_stats {
   int32_t split;           /* 1: the traceback is split at strip boundaries (few long pairs) */
   int32_t grouped;         /* pair groups of the grouped DP (four short reads per wave sharing one
                               reference), 0: one wave per pair */
+  int32_t group_pairs;     /* pairs per wave of the grouped DP (4 or 2), 0: not grouped */
 } bg_stats;
 
 int bg_get_stats(bg_aligner* h, bg_stats* out);

@@ -83,7 +83,7 @@ def test_C4_reads_vs_refs_slice(aligner, oracle):
     st = aligner.stats()
     assert st["tagged"] == 1 and st["checkpoint"] == 1 and st["wide"] == 0, st
     # four reads of one reference per wave (bg_grp_kernel.hip), the walker recomputing alone
-    assert st["grouped"] == 8 * 32 and st["R"] == 10, st
+    assert st["grouped"] == 8 * 32 and st["group_pairs"] == 4 and st["R"] == 10, st
     assert (st["fin_waves"], st["fin_slots"]) == (1, 6), st
     assert all(r.status == 0 for r in res)
     # 150 bp reads against 10 kbp refs: the row branch (end cell in the last row)

@@ -1,9 +1,10 @@
-"""Grouped DP (bg_grp_kernel.hip, round 5): short reads that share a reference run four to a wave,
-one per 16-lane DPP row, and the traceback recomputes a pair's chunks as 16-lane jobs
-(bg_finish.h recompute_grp).  Results must not change: score and both strings against the
-oracle, and identical to the one-wave-per-pair path (BG_GROUPED=0) over whole batches, at every
-R the planner picks (16 R >= the longest read), in the four linear-path modes, with references
-shorter than a chunk, one column long, and groups with empty rows."""
+"""Grouped DP (bg_grp_kernel.hip, round 5): short reads that share a reference run P to a wave
+(P = 4: one per 16-lane DPP row; P = 2: 32 lanes each), and the traceback recomputes a pair's
+chunks as 64 / P-lane jobs (bg_finish.h recompute_grp).  Results must not change: score and both
+strings against the oracle, and identical to the one-wave-per-pair path (BG_GROUPED=0) over
+whole batches, at both P and every R the planner picks ((64 / P) R >= the longest read), in the
+four linear-path modes, with references shorter than a chunk, one column long, and groups with
+empty rows."""
 import os
 import random
 
@@ -14,32 +15,41 @@ from parity_util import DNA, check_batch, check_results, mutate, rand_seq, sampl
 pytestmark = pytest.mark.gpu
 
 
-def _align(mode, pairs, a, b, grouped):
+def _align(mode, pairs, a, b, grouped, P=""):
     from biogarden_amd.alignment import score
     from biogarden_amd.alignment.aligner import SequenceAligner
-    old = os.environ.get("BG_GROUPED")
-    os.environ["BG_GROUPED"] = grouped
+    env = {"BG_GROUPED": grouped, "BG_GRP_P": P}
+    old = {k: os.environ.get(k) for k in env}
+    for k, v in env.items():
+        if v:
+            os.environ[k] = v
+        else:
+            os.environ.pop(k, None)
     al = SequenceAligner(0)
     try:
         res = al.align_batch(mode, pairs, score.blosum62, a, b)
         return res, al.stats()
     finally:
         al.close()
-        if old is None:
-            del os.environ["BG_GROUPED"]
-        else:
-            os.environ["BG_GROUPED"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _key(r):
     return (r.status, r[0], bytes(r[1].chain), bytes(r[2].chain))
 
 
-def test_grouped_C4_slice_matches_ungrouped(oracle):
+@pytest.mark.parametrize("P", ["4", "2"])
+def test_grouped_C4_slice_matches_ungrouped(oracle, P):
     from tools import workloads as w
-    pairs = w.c4_pairs(nrefs=8, reads_per_ref=130)          # 130 per reference: a partial group
-    res, st = _align("semiglobal", pairs, -1, -2, "")
-    assert st["grouped"] == 8 * 33 and st["R"] == 10 and st["checkpoint"] == 1, st
+    pairs = w.c4_pairs(nrefs=8, reads_per_ref=131)          # 131 per reference: partial groups
+    res, st = _align("semiglobal", pairs, -1, -2, "", P)
+    ng = 8 * ((131 + int(P) - 1) // int(P))
+    assert st["grouped"] == ng and st["group_pairs"] == int(P) and st["checkpoint"] == 1, st
+    assert st["R"] == (10 if P == "4" else 5), st
     assert (st["fin_waves"], st["fin_slots"]) == (1, 6), st
     ref, st0 = _align("semiglobal", pairs, -1, -2, "0")
     assert st0["grouped"] == 0, st0
@@ -50,9 +60,9 @@ def test_grouped_C4_slice_matches_ungrouped(oracle):
     assert all(r.status == 0 and r.end[0] == 150 for r in res)
 
 
-def _edge_pairs(seed, R, mode):
+def _edge_pairs(seed, R, mode, P):
     rng = random.Random(seed)
-    top = 16 * R
+    top = (64 // P) * R
     reflens = [1, 5, 63, 64, 65, 127, 200, 700]
     if mode == "fitting":                                   # seq2 fits in seq1 (n2 <= n1)
         reflens = [1, 2, 5, max(1, top // 4), max(1, top // 2), top - 1, top]
@@ -62,6 +72,7 @@ def _edge_pairs(seed, R, mode):
         lo = n2 if mode == "fitting" else 1
         lens = [lo, top, top - 1, max(lo, top - 15), max(lo, top // 2), rng.randint(lo, top), rng.randint(lo, top)]
         for n1 in lens[:5 + (n2 % 3)]:                      # 5 .. 7 reads: groups with empty rows
+            n1 = max(n1, lo)
             if n2 > n1 and rng.random() < 0.6:
                 o = rng.randint(0, n2 - n1)
                 read = (mutate(rng, ref[o:o + n1], DNA, 0.1) + rand_seq(rng, n1, DNA))[:n1]
@@ -74,13 +85,14 @@ def _edge_pairs(seed, R, mode):
     return pairs
 
 
+@pytest.mark.parametrize("P", [4, 2])
 @pytest.mark.parametrize("R", [2, 3, 5, 8, 10])
 @pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("global", -2, -2), ("fitting", -1, -1),
                                       ("overlap", -1, -3)])
-def test_grouped_edges_vs_oracle(oracle, R, mode, a, b):
-    pairs = _edge_pairs(1000 * R + len(mode), R, mode)
-    res, st = _align(mode, pairs, a, b, "1")
-    assert st["grouped"] > 0 and st["R"] == R, st
+def test_grouped_edges_vs_oracle(oracle, R, mode, a, b, P):
+    pairs = _edge_pairs(1000 * R + 10 * P + len(mode), R, mode, P)
+    res, st = _align(mode, pairs, a, b, "1", str(P))
+    assert st["grouped"] > 0 and st["group_pairs"] == P and st["R"] == R, st
     check_results(oracle, mode, pairs, res, "blosum62", a, b)
     ref, _ = _align(mode, pairs, a, b, "0")
     diff = [p for p in range(len(pairs)) if _key(res[p]) != _key(ref[p])]
