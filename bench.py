@@ -141,6 +141,9 @@ def workload_name(mode, npairs, n1, n2, a, b):
 
 
 def kernel_name(st):
+    if st.get("grouped"):
+        return "bg_dp_grp_kernel<R=%d,P=%d> (%d groups of %d reads per wave)" % (
+            st["R"], st["group_pairs"], st["grouped"], st["group_pairs"])
     if st["tagged"]:
         return "bg_dp_tag_kernel<R=%d,%s,ckpt=%d>" % (st["R"], "WIDE" if st["wide"] else "strips",
                                                      st["checkpoint"])
@@ -150,6 +153,8 @@ def kernel_name(st):
 
 
 def finish_name(st):
+    if st.get("grouped"):
+        return "bg_finish_kernel<R=%d,checkpoint,grouped P=%d>" % (st["R"], st["group_pairs"])
     if st.get("split"):
         return "split traceback (bg_exit_kernel<R=%d> + bg_finish_kernel phases)" % st["R"]
     return "bg_finish_kernel<R=%d,%s>" % (st["R"], "checkpoint" if st["checkpoint"] else "trace")
@@ -344,7 +349,8 @@ def kernel_info(st, pipeline):
     return {"R": st["R"], "waves": st["waves"], "affine": st["affine"], "tagged": st["tagged"],
             "checkpoint": st["checkpoint"], "wide": st["wide"], "split": st.get("split", 0),
             "dna_profile": st["dna"],
-            "pipeline": pipeline, "fin_waves": st["fin_waves"], "fin_slots": st["fin_slots"]}
+            "pipeline": pipeline, "fin_waves": st["fin_waves"], "fin_slots": st["fin_slots"],
+            "grouped": st.get("grouped", 0), "group_pairs": st.get("group_pairs", 0)}
 
 
 # K for the configs legs: the metric's default (20) for every configuration, so that each leg's
