@@ -28,7 +28,7 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_fasta_close", "bg_split_stats", "bg_split_conc_diag", "bg_aligner_new_shared",
            "bg_set_async_fetch", "bg_group_new", "bg_group_free", "bg_group_size",
            "bg_group_member", "bg_group_align_batch", "bg_group_plan", "bg_group_buffer_size",
-           "bg_group_timing"]
+           "bg_group_timing", "bg_group_submit", "bg_group_collect", "bg_group_pending"]
 
 
 class NativeUnavailable(RuntimeError):
@@ -164,6 +164,10 @@ def lib():
     L.bg_group_member.restype = ctypes.c_void_p
     L.bg_group_align_batch.argtypes = [ctypes.c_void_p] + batch_args[1:] + [
         ctypes.POINTER(BgPairResult), c_u8p, c_u8p, ctypes.c_size_t]
+    L.bg_group_submit.argtypes = [ctypes.c_void_p] + batch_args[1:]
+    L.bg_group_collect.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
+                                   ctypes.c_size_t]
+    L.bg_group_pending.argtypes = [ctypes.c_void_p]
     L.bg_group_plan.argtypes = [ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
                                 ctypes.POINTER(ctypes.c_size_t), ctypes.c_int,
                                 ctypes.POINTER(ctypes.c_int32)]
@@ -495,6 +499,27 @@ class Group:
                         "aligned2": b2[lo:hi], "end": (r.end_i, r.end_j),
                         "start": (r.start1, r.start2)})
         return out
+
+    def submit(self, mode, pairs, scoring, a, b):
+        """bg_group_submit: queue one batch (at most three in flight); returns a ticket that
+        collect() consumes in submission order.  The ticket holds the sequence buffers alive."""
+        a1, n1, a2, n2, total = Handle._arrays(pairs)
+        check(lib().bg_group_submit(self._p, MODES.get(mode, mode), len(pairs), a1, n1, a2, n2,
+                                    ctypes.byref(scoring), a, b))
+        return (a1, n1, a2, n2, total, len(pairs), pairs)
+
+    def collect(self, ticket):
+        """bg_group_collect for the oldest submitted batch (pass its ticket): -> (results, out1,
+        out2) as align_batch_raw."""
+        total, n = ticket[4], ticket[5]
+        res = (BgPairResult * max(n, 1))()
+        o1 = (ctypes.c_uint8 * max(total, 1))()
+        o2 = (ctypes.c_uint8 * max(total, 1))()
+        check(lib().bg_group_collect(self._p, res, o1, o2, total))
+        return res, o1, o2
+
+    def pending(self):
+        return lib().bg_group_pending(self._p)
 
     def buffer_size(self):
         r, c = ctypes.c_size_t(), ctypes.c_size_t()

@@ -19,6 +19,13 @@
 //      offsets (bgh::compact_expand), exactly the layout bg_align_batch returns.
 // Members on one device share that device's HIP streams (bg_aligner_new_shared), so their DPs and
 // tracebacks pipeline as consecutive executes of one handle do.
+// bg_group_submit / bg_group_collect split a call in two so that kGSlots batches are in flight:
+// every member has kGSlots aligners (pipeline slots), a submit runs steps 1-3 up to the executes
+// and returns, a collect runs the exports, 4 and 5 of the oldest batch.  Three: while the host
+// collects batch k (its traceback, then ~1 ms of expansion), k + 1 and k + 2 keep the device's
+// DP stream busy (two left it idle for the expansion: M 6 500 GCUPS against 4 608 synchronous).  While one batch's DPs and
+// tracebacks run on the devices, the host prepares the next and expands the previous, and the
+// devices overlap one batch's tracebacks with the next one's DPs.
 //
 // librccl is opened at bg_group_new (dlopen), not linked: a process that never groups devices
 // does not load it, and one that already holds torch's copy reuses it.
@@ -32,13 +39,18 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <thread>
 #include <type_traits>
 #include <vector>
 
+#include "bg_device.h"
 #include "bg_host_passes.h"
 #include "biogarden_gpu.h"
+
+extern "C" void* bg_aligner_aux_stream(bg_aligner* h);   // bg_host.cpp
+extern "C" void* bg_download_kernel_ptr();                // bg_io.hip
 
 namespace {
 
@@ -85,19 +97,36 @@ double ms_since(std::chrono::steady_clock::time_point& t) {
 }  // namespace
 
 enum { kGPrepExec, kGExport, kGGather, kGDownload, kGExpand, kGN };
+constexpr int kGSlots = 3;       // batches in flight (submitted, not collected)
+
+// one submitted batch: the caller's pair arrays (copied; the sequence bytes stay the caller's
+// until the collect), the shards, and the slot its members' aligners run it on
+struct GBatch {
+  int slot = 0;
+  size_t npairs = 0;
+  std::vector<const uint8_t*> s1, s2;
+  std::vector<size_t> n1, n2;
+  std::vector<uint64_t> coff;
+  uint64_t need = 0;
+  std::vector<std::vector<size_t>> idx;   // member -> its pairs (caller indices)
+};
 
 struct bg_group {
   std::vector<int> dev;            // member -> HIP device
-  std::vector<bg_aligner*> h;      // member -> aligner
+  std::vector<bg_aligner*> h;      // (member, slot) -> aligner, at kGSlots m + slot
   std::vector<int> rankDev;        // communicator rank -> device (rank 0: member 0's device)
   std::vector<int> rankOf;         // member -> rank
   std::vector<ncclComm_t> comm;    // per rank
-  std::vector<hipStream_t> cs;     // per rank: the gather's stream
-  std::vector<void*> ebuf;         // member -> its compact record (on its device)
+  std::vector<hipStream_t> cs;     // per rank: the gather's stream (its device's shared download
+                                   // stream, owned by the members' aligners)
+  std::vector<void*> ebuf;         // (member, slot) -> its compact record (on its device)
   std::vector<size_t> ecap;
+  std::deque<GBatch> pending;      // submitted, not yet collected (at most kGSlots)
+  int nextSlot = 0;
   void* gbuf = nullptr;            // the gathered records, on the root device
   size_t gcap = 0;
-  void* hbuf = nullptr;            // ... downloaded (pinned)
+  void* hbuf = nullptr;            // ... downloaded (pinned, host-mapped: a kernel writes it)
+  void* hdev = nullptr;            // hbuf's device address
   size_t hcap = 0;
   long rows = 1024, cols = 1024;   // the reference aligner's scratch dims (the group is ONE aligner)
   int rcclSelf = 0;                // BG_GROUP_RCCL_SELF=1: root-device members go through RCCL too
@@ -120,10 +149,8 @@ extern "C" void bg_group_free(bg_group* g) {
   if (!g) return;
   for (size_t r = 0; r < g->comm.size(); ++r)
     if (g->comm[r]) (void)rccl().commDestroy(g->comm[r]);
-  for (size_t r = 0; r < g->cs.size(); ++r)
-    if (g->cs[r]) { (void)hipSetDevice(g->rankDev[r]); (void)hipStreamDestroy(g->cs[r]); }
-  for (size_t m = 0; m < g->ebuf.size(); ++m)
-    if (g->ebuf[m]) { (void)hipSetDevice(g->dev[m]); (void)hipFree(g->ebuf[m]); }
+  for (size_t x = 0; x < g->ebuf.size(); ++x)
+    if (g->ebuf[x]) { (void)hipSetDevice(g->dev[x / kGSlots]); (void)hipFree(g->ebuf[x]); }
   if (g->gbuf) { (void)hipSetDevice(g->rankDev[0]); (void)hipFree(g->gbuf); }
   if (g->hbuf) (void)hipHostFree(g->hbuf);
   // members sharing a device's streams: the stream owner (the first on its device) goes last
@@ -141,29 +168,31 @@ extern "C" bg_group* bg_group_new(const int* devices, int n) {
   if (!rccl().ok) return nullptr;
   bg_group* g = new bg_group();
   g->dev.assign(devices, devices + n);
-  g->h.assign(n, nullptr);
+  g->h.assign(kGSlots * n, nullptr);
   g->rankOf.assign(n, -1);
   for (int m = 0; m < n; ++m) {
     int r = 0;
     while (r < (int)g->rankDev.size() && g->rankDev[r] != devices[m]) ++r;
     if (r == (int)g->rankDev.size()) g->rankDev.push_back(devices[m]);
     g->rankOf[m] = r;
-    // the first member on a device owns its streams; the others share them
+    // the first member on a device owns its streams (its slot-0 aligner); every other aligner on
+    // the device shares them
     int first = 0;
     while (g->dev[first] != devices[m]) ++first;
-    g->h[m] = first == m ? bg_aligner_new(devices[m]) : bg_aligner_new_shared(g->h[first]);
-    if (!g->h[m] || bg_set_pipeline(g->h[m], 2) != BG_OK) { bg_group_free(g); return nullptr; }
+    for (int sl = 0; sl < kGSlots; ++sl) {
+      bg_aligner*& hh = g->h[kGSlots * m + sl];
+      hh = (first == m && sl == 0) ? bg_aligner_new(devices[m]) : bg_aligner_new_shared(g->h[kGSlots * first]);
+      if (!hh || bg_set_pipeline(hh, 2) != BG_OK) { bg_group_free(g); return nullptr; }
+    }
   }
   const int nr = (int)g->rankDev.size();
   g->comm.assign(nr, nullptr);
   g->cs.assign(nr, nullptr);
   for (int r = 0; r < nr; ++r) {
-    if (hipSetDevice(g->rankDev[r]) != hipSuccess ||
-        hipStreamCreateWithFlags(&g->cs[r], hipStreamNonBlocking) != hipSuccess) {
-      g->cs[r] = nullptr;
-      bg_group_free(g);
-      return nullptr;
-    }
+    int first = 0;
+    while (g->dev[first] != g->rankDev[r]) ++first;
+    g->cs[r] = static_cast<hipStream_t>(bg_aligner_aux_stream(g->h[kGSlots * first]));
+    if (!g->cs[r]) { bg_group_free(g); return nullptr; }
   }
   const ncclResult_t rc = rccl().commInitAll(g->comm.data(), nr, g->rankDev.data());
   if (rc != ncclSuccess) {
@@ -172,17 +201,17 @@ extern "C" bg_group* bg_group_new(const int* devices, int n) {
     bg_group_free(g);
     return nullptr;
   }
-  g->ebuf.assign(n, nullptr);
-  g->ecap.assign(n, 0);
+  g->ebuf.assign(kGSlots * n, nullptr);
+  g->ecap.assign(kGSlots * n, 0);
   const char* e = std::getenv("BG_GROUP_RCCL_SELF");
   g->rcclSelf = e && e[0] == '1';
   return g;
 }
 
-extern "C" int bg_group_size(const bg_group* g) { return g ? (int)g->h.size() : BG_E_ARG; }
+extern "C" int bg_group_size(const bg_group* g) { return g ? (int)g->dev.size() : BG_E_ARG; }
 
 extern "C" bg_aligner* bg_group_member(bg_group* g, int m) {
-  return (g && m >= 0 && m < (int)g->h.size()) ? g->h[m] : nullptr;
+  return (g && m >= 0 && m < (int)g->dev.size()) ? g->h[kGSlots * m] : nullptr;
 }
 
 extern "C" int bg_group_plan(size_t npairs, const size_t* n1, const size_t* n2, int nshards,
@@ -210,39 +239,40 @@ extern "C" int bg_group_timing(bg_group* g, double* ms, size_t n, uint64_t* call
   return kGN;
 }
 
-extern "C" int bg_group_align_batch(bg_group* g, int mode, size_t npairs, const uint8_t* const* s1,
-                                    const size_t* n1, const uint8_t* const* s2, const size_t* n2,
-                                    const bg_scoring* sc, int32_t a, int32_t b, bg_pair_result* res,
-                                    uint8_t* out1, uint8_t* out2, size_t out_cap) {
-  if (!g || !sc || mode < BG_GLOBAL || mode > BG_SEMIGLOBAL) return BG_E_ARG;
-  if (npairs && (!s1 || !n1 || !s2 || !n2 || !res)) return BG_E_ARG;
-  uint64_t need = 0;
-  std::vector<uint64_t> coff(npairs);
-  for (size_t p = 0; p < npairs; ++p) {
-    coff[p] = need;
-    need += (uint64_t)n1[p] + n2[p];
-  }
-  if (need && (!out1 || !out2 || out_cap < need)) return BG_E_ARG;
+extern "C" int bg_group_submit(bg_group* g, int mode, size_t npairs, const uint8_t* const* s1,
+                               const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                               const bg_scoring* sc, int32_t a, int32_t b) {
+  if (!g || !sc || mode < BG_GLOBAL || mode > BG_SEMIGLOBAL || g->pending.size() >= (size_t)kGSlots) return BG_E_ARG;
+  if (npairs && (!s1 || !n1 || !s2 || !n2)) return BG_E_ARG;
   auto t = std::chrono::steady_clock::now();
-  ++g->calls;
-  const int M = (int)g->h.size();
-  // 1-2: the shards and every call's scratch dims (the group's dims move on only if the batch runs)
+  const int M = (int)g->dev.size();
+  GBatch B;
+  B.slot = g->nextSlot;
+  B.npairs = npairs;
+  B.s1.assign(s1, s1 + npairs);
+  B.s2.assign(s2, s2 + npairs);
+  B.n1.assign(n1, n1 + npairs);
+  B.n2.assign(n2, n2 + npairs);
+  B.coff.resize(npairs);
+  for (size_t p = 0; p < npairs; ++p) {
+    B.coff[p] = B.need;
+    B.need += (uint64_t)n1[p] + n2[p];
+  }
+  // 1-2: the shards and every call's scratch dims (the group's dims move on with each submit)
   std::vector<int32_t> shardOf(npairs);
   bgh::lpt_plan(npairs, n1, n2, M, shardOf.data());
   long rows = g->rows, cols = g->cols;
   std::vector<std::pair<long, long>> dims;
   bgh::batch_call_dims(mode, npairs, n1, n2, a, b, rows, cols, dims);
-  std::vector<std::vector<size_t>> idx(M);
-  for (size_t p = 0; p < npairs; ++p) idx[shardOf[p]].push_back(p);
-  // 3: every member prepares, executes and packs its shard (one host thread each)
+  B.idx.assign(M, {});
+  for (size_t p = 0; p < npairs; ++p) B.idx[shardOf[p]].push_back(p);
+  // 3 (first half): every member prepares and executes its shard (one host thread each)
   std::vector<int> rc(M, BG_OK);
-  std::vector<size_t> size(M, 0);
-  std::vector<double> tExp(M, 0.0);
   auto member = [&](int m) {
-    const std::vector<size_t>& I = idx[m];
+    const std::vector<size_t>& I = B.idx[m];
     const size_t k = I.size();
     if (!k) return;
-    bg_aligner* h = g->h[m];
+    bg_aligner* h = g->h[kGSlots * m + B.slot];
     std::vector<const uint8_t*> p1(k), p2(k);
     std::vector<size_t> l1(k), l2(k);
     std::vector<uint64_t> r(k), c(k);
@@ -254,20 +284,6 @@ extern "C" int bg_group_align_batch(bg_group* g, int mode, size_t npairs, const 
     int e = bg_aligner_set_call_dims(h, k, r.data(), c.data());
     if (!e) e = bg_batch_prepare(h, mode, k, p1.data(), l1.data(), p2.data(), l2.data(), sc, a, b);
     if (!e) e = bg_batch_execute(h);
-    auto t1 = std::chrono::steady_clock::now();
-    size_t sz = 0;
-    if (!e) e = bg_batch_export_compact(h, nullptr, &sz);
-    if (!e && g->ecap[m] < sz) {
-      (void)hipSetDevice(g->dev[m]);
-      if (g->ebuf[m]) (void)hipFree(g->ebuf[m]);
-      g->ebuf[m] = nullptr;
-      g->ecap[m] = 0;
-      if (hipMalloc(&g->ebuf[m], sz + sz / 4) != hipSuccess) { g->ebuf[m] = nullptr; e = BG_E_NOMEM; }
-      else g->ecap[m] = sz + sz / 4;
-    }
-    if (!e) e = bg_batch_export_compact(h, g->ebuf[m], &sz);
-    tExp[m] = ms_since(t1);
-    size[m] = sz;
     rc[m] = e;
   };
   {
@@ -278,21 +294,69 @@ extern "C" int bg_group_align_batch(bg_group* g, int mode, size_t npairs, const 
   }
   for (int m = 0; m < M; ++m)
     if (rc[m]) return rc[m];
-  const double tAll = ms_since(t);
-  const double tE = *std::max_element(tExp.begin(), tExp.end());
-  g->ms[kGPrepExec] += tAll - tE;
-  g->ms[kGExport] += tE;
+  g->rows = rows;
+  g->cols = cols;
+  g->nextSlot = (g->nextSlot + 1) % kGSlots;
+  g->pending.push_back(std::move(B));
+  g->ms[kGPrepExec] += ms_since(t);
+  return BG_OK;
+}
+
+extern "C" int bg_group_collect(bg_group* g, bg_pair_result* res, uint8_t* out1, uint8_t* out2,
+                                size_t out_cap) {
+  if (!g || g->pending.empty()) return BG_E_ARG;
+  const GBatch& B = g->pending.front();
+  if (B.npairs && !res) return BG_E_ARG;
+  if (B.need && (!out1 || !out2 || out_cap < B.need)) return BG_E_ARG;
+  auto t = std::chrono::steady_clock::now();
+  ++g->calls;
+  const int M = (int)g->dev.size();
+  // 3 (second half): every member's wait and compact export (one host thread each)
+  std::vector<int> rc(M, BG_OK);
+  std::vector<size_t> size(M, 0);
+  auto member = [&](int m) {
+    if (B.idx[m].empty()) return;
+    const int x = kGSlots * m + B.slot;
+    bg_aligner* h = g->h[x];
+    size_t sz = 0;
+    int e = bg_batch_export_compact(h, nullptr, &sz);
+    if (!e && g->ecap[x] < sz) {
+      (void)hipSetDevice(g->dev[m]);
+      if (g->ebuf[x]) (void)hipFree(g->ebuf[x]);
+      g->ebuf[x] = nullptr;
+      g->ecap[x] = 0;
+      if (hipMalloc(&g->ebuf[x], sz + sz / 4) != hipSuccess) { g->ebuf[x] = nullptr; e = BG_E_NOMEM; }
+      else g->ecap[x] = sz + sz / 4;
+    }
+    if (!e) e = bg_batch_export_compact(h, g->ebuf[x], &sz);
+    size[m] = sz;
+    rc[m] = e;
+  };
+  {
+    std::vector<std::thread> th;
+    for (int m = 1; m < M; ++m) th.emplace_back(member, m);
+    member(0);
+    for (auto& x : th) x.join();
+  }
+  int err = BG_OK;
+  for (int m = 0; m < M && !err; ++m) err = rc[m];
+  auto finish = [&](int e) {
+    g->pending.pop_front();
+    return e;
+  };
+  if (err) return finish(err);
+  g->ms[kGExport] += ms_since(t);
   // 4: the gather into one buffer on the root device
   std::vector<uint64_t> goff(M + 1, 0);
   for (int m = 0; m < M; ++m) goff[m + 1] = goff[m] + size[m];
   const int root = g->rankDev[0];
   hipError_t he;
   if (goff[M] > g->gcap) {
-    if ((he = hipSetDevice(root)) != hipSuccess) return hip_fail(he, "hipSetDevice");
+    if ((he = hipSetDevice(root)) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
     if (g->gbuf) (void)hipFree(g->gbuf);
     g->gbuf = nullptr;
     g->gcap = 0;
-    if (hipMalloc(&g->gbuf, goff[M] + goff[M] / 4) != hipSuccess) { g->gbuf = nullptr; return BG_E_NOMEM; }
+    if (hipMalloc(&g->gbuf, goff[M] + goff[M] / 4) != hipSuccess) { g->gbuf = nullptr; return finish(BG_E_NOMEM); }
     g->gcap = goff[M] + goff[M] / 4;
   }
   uint8_t* gb = static_cast<uint8_t*>(g->gbuf);
@@ -301,71 +365,103 @@ extern "C" int bg_group_align_batch(bg_group* g, int mode, size_t npairs, const 
     if (size[m] && (g->rankOf[m] != 0 || g->rcclSelf)) viaRccl = true;
   for (int m = 0; m < M; ++m)
     if (size[m] && g->rankOf[m] == 0 && !g->rcclSelf) {
-      if ((he = hipSetDevice(root)) != hipSuccess) return hip_fail(he, "hipSetDevice");
-      if ((he = hipMemcpyAsync(gb + goff[m], g->ebuf[m], size[m], hipMemcpyDeviceToDevice, g->cs[0])) != hipSuccess)
-        return hip_fail(he, "gather copy");
+      if ((he = hipSetDevice(root)) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
+      if ((he = hipMemcpyAsync(gb + goff[m], g->ebuf[kGSlots * m + B.slot], size[m], hipMemcpyDeviceToDevice,
+                               g->cs[0])) != hipSuccess)
+        return finish(hip_fail(he, "gather copy"));
     }
   if (viaRccl) {
     const Rccl& R = rccl();
     ncclResult_t nr = R.groupStart();
-    if (nr != ncclSuccess) return nccl_fail(nr, "ncclGroupStart");
+    if (nr != ncclSuccess) return finish(nccl_fail(nr, "ncclGroupStart"));
     // per member in member order: its rank sends, the root receives (NCCL matches each pair of
     // ranks' sends and receives in issue order)
     for (int m = 0; m < M && nr == ncclSuccess; ++m) {
       if (!size[m] || (g->rankOf[m] == 0 && !g->rcclSelf)) continue;
       const int r = g->rankOf[m];
-      nr = R.send(g->ebuf[m], size[m], ncclUint8, 0, g->comm[r], g->cs[r]);
+      nr = R.send(g->ebuf[kGSlots * m + B.slot], size[m], ncclUint8, 0, g->comm[r], g->cs[r]);
       if (nr == ncclSuccess) nr = R.recv(gb + goff[m], size[m], ncclUint8, r, g->comm[0], g->cs[0]);
     }
     const ncclResult_t ne = R.groupEnd();
-    if (nr != ncclSuccess) return nccl_fail(nr, "ncclSend / ncclRecv");
-    if (ne != ncclSuccess) return nccl_fail(ne, "ncclGroupEnd");
+    if (nr != ncclSuccess) return finish(nccl_fail(nr, "ncclSend / ncclRecv"));
+    if (ne != ncclSuccess) return finish(nccl_fail(ne, "ncclGroupEnd"));
   }
   for (size_t r = 1; r < g->cs.size(); ++r) {
-    if ((he = hipSetDevice(g->rankDev[r])) != hipSuccess) return hip_fail(he, "hipSetDevice");
-    if ((he = hipStreamSynchronize(g->cs[r])) != hipSuccess) return hip_fail(he, "gather (send side)");
+    if ((he = hipSetDevice(g->rankDev[r])) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
+    if ((he = hipStreamSynchronize(g->cs[r])) != hipSuccess) return finish(hip_fail(he, "gather (send side)"));
   }
-  if ((he = hipSetDevice(root)) != hipSuccess) return hip_fail(he, "hipSetDevice");
-  if ((he = hipStreamSynchronize(g->cs[0])) != hipSuccess) return hip_fail(he, "gather");
+  if ((he = hipSetDevice(root)) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
+  if ((he = hipStreamSynchronize(g->cs[0])) != hipSuccess) return finish(hip_fail(he, "gather"));
   g->ms[kGGather] += ms_since(t);
-  // 5: one download, then the expansion into the caller's buffers at the caller's offsets
+  // 5: one download, then the expansion into the caller's buffers at the caller's offsets.  The
+  // download is a kernel writing host-mapped pinned memory (bg_download_kernel), as the handles'
+  // asynchronous fetch: a hipMemcpyAsync device-to-host under the HIP runtime torch loads waits
+  // for the device's other queued work (1.7 ms of a 3.8 ms pipelined M batch)
   if (goff[M] > g->hcap) {
     if (g->hbuf) (void)hipHostFree(g->hbuf);
     g->hbuf = nullptr;
+    g->hdev = nullptr;
     g->hcap = 0;
-    if (hipHostMalloc(&g->hbuf, goff[M] + goff[M] / 4, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(&g->hbuf, goff[M] + goff[M] / 4, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess ||
+        hipHostGetDevicePointer(&g->hdev, g->hbuf, 0) != hipSuccess) {
+      if (g->hbuf) (void)hipHostFree(g->hbuf);
       g->hbuf = nullptr;
-      return BG_E_NOMEM;
+      g->hdev = nullptr;
+      return finish(BG_E_NOMEM);
     }
     g->hcap = goff[M] + goff[M] / 4;
   }
   if (goff[M]) {
-    if ((he = hipMemcpyAsync(g->hbuf, g->gbuf, goff[M], hipMemcpyDeviceToHost, g->cs[0])) != hipSuccess ||
+    BgDownloadArgs D;
+    std::memset(&D, 0, sizeof(D));
+    D.seg[0] = {static_cast<const uint8_t*>(g->gbuf), static_cast<uint8_t*>(g->hdev), goff[M]};
+    D.nseg = 1;
+    const unsigned blocks = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(64, (goff[M] / 16 + 255) / 256));
+    void* dargs[] = {&D};
+    if ((he = hipLaunchKernel(bg_download_kernel_ptr(), dim3(blocks), dim3(256), dargs, 0, g->cs[0])) != hipSuccess ||
         (he = hipStreamSynchronize(g->cs[0])) != hipSuccess)
-      return hip_fail(he, "download");
+      return finish(hip_fail(he, "download"));
   }
   g->ms[kGDownload] += ms_since(t);
   const uint8_t* hb = static_cast<const uint8_t*>(g->hbuf);
   for (int m = 0; m < M; ++m) {
-    const std::vector<size_t>& I = idx[m];
+    const std::vector<size_t>& I = B.idx[m];
     const size_t k = I.size();
     if (!k) continue;
     std::vector<const uint8_t*> p1(k), p2(k);
     std::vector<size_t> l1(k), l2(k);
     std::vector<uint64_t> dst(k);
     for (size_t q = 0; q < k; ++q) {
-      p1[q] = s1[I[q]]; l1[q] = n1[I[q]];
-      p2[q] = s2[I[q]]; l2[q] = n2[I[q]];
-      dst[q] = coff[I[q]];
+      p1[q] = B.s1[I[q]]; l1[q] = B.n1[I[q]];
+      p2[q] = B.s2[I[q]]; l2[q] = B.n2[I[q]];
+      dst[q] = B.coff[I[q]];
     }
     std::vector<bg_pair_result> rm(k);
     const int e = bgh::compact_expand(hb + goff[m], size[m], k, p1.data(), l1.data(), p2.data(), l2.data(),
                                       rm.data(), out1, out2, out_cap, dst.data());
-    if (e) return e;
+    if (e) return finish(e);
     for (size_t q = 0; q < k; ++q) res[I[q]] = rm[q];
   }
   g->ms[kGExpand] += ms_since(t);
-  g->rows = rows;
-  g->cols = cols;
-  return BG_OK;
+  return finish(BG_OK);
+}
+
+extern "C" int bg_group_pending(const bg_group* g) { return g ? (int)g->pending.size() : BG_E_ARG; }
+
+extern "C" int bg_group_align_batch(bg_group* g, int mode, size_t npairs, const uint8_t* const* s1,
+                                    const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                                    const bg_scoring* sc, int32_t a, int32_t b, bg_pair_result* res,
+                                    uint8_t* out1, uint8_t* out2, size_t out_cap) {
+  if (!g || !g->pending.empty()) return BG_E_ARG;
+  if (npairs && (!s1 || !n1 || !s2 || !n2 || !res)) return BG_E_ARG;
+  uint64_t need = 0;
+  for (size_t p = 0; p < npairs; ++p) need += (uint64_t)n1[p] + n2[p];
+  if (need && (!out1 || !out2 || out_cap < need)) return BG_E_ARG;
+  // the dims move on only if the batch runs: a failed collect restores them
+  const long rows = g->rows, cols = g->cols;
+  int e = bg_group_submit(g, mode, npairs, s1, n1, s2, n2, sc, a, b);
+  if (e) return e;
+  e = bg_group_collect(g, res, out1, out2, out_cap);
+  if (e) { g->rows = rows; g->cols = cols; }
+  return e;
 }

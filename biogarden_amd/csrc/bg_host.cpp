@@ -509,6 +509,16 @@ static void note_hip(hipError_t e, const char* what, int line) {
 
 extern "C" int bg_last_hip_error(void) { return g_lastHip; }
 
+// bg_group (bg_group.cpp, not a public entry point): the stream a handle's device shares for
+// downloads and exports, so the group's gather queues there instead of on a stream of its own (a
+// fifth stream shares a hardware queue with the DP stream at the box's 4 queues, and its copies
+// wait behind the DPs queued there)
+extern "C" void* bg_aligner_aux_stream(bg_aligner* h) {
+  if (!h || hipSetDevice(h->device) != hipSuccess) return nullptr;
+  if (!h->dlS) h->dlS = group_stream(h, kSDl);
+  return (void*)h->dlS;
+}
+
 extern "C" int bg_set_async_fetch(bg_aligner* h, int on) {
   if (!h) return BG_E_ARG;
   BG_HIP(drain(h));
@@ -2196,18 +2206,27 @@ extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) 
   E.nplan = (int32_t)h->plan.size();
   E.mode = h->mode;
   void* args[] = {&E};
+  // a handle sharing its device's streams exports on the shared download stream: on the DP stream
+  // the export would queue behind the DPs other handles queued after this batch's (bg_group with
+  // three batches in flight waited for two more DPs per collect)
+  hipStream_t xs = h->stream;
+  if (h->shared()) {
+    if (!h->dlS) h->dlS = group_stream(h, kSDl);
+    if (!h->dlS) return BG_E_HIP;
+    xs = h->dlS;
+  }
   if (h->compactExec != h->execCount) {
     // sizes and their scan for this execute (after its traceback), then the total to the host
     if (!h->compactSizes.ensure(8 * (n + 1))) return BG_E_NOMEM;
     E.sizes = h->compactSizes.as<uint64_t>();
     E.dst = nullptr;
     BG_HIP(drain(h));
-    BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), h->stream));
+    BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), xs));
     const unsigned g = (unsigned)(((uint64_t)E.nplan + 255) / 256);
-    if (g) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(g), dim3(256), args, 0, h->stream));
-    BG_HIP(hipLaunchKernel(bg_compact_scan_kernel_ptr(), dim3(1), dim3(1024), args, 0, h->stream));
-    BG_HIP(hipMemcpyAsync(&h->compactOps, E.sizes + n, 8, hipMemcpyDeviceToHost, h->stream));
-    BG_HIP(hipStreamSynchronize(h->stream));
+    if (g) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(g), dim3(256), args, 0, xs));
+    BG_HIP(hipLaunchKernel(bg_compact_scan_kernel_ptr(), dim3(1), dim3(1024), args, 0, xs));
+    BG_HIP(hipMemcpyAsync(&h->compactOps, E.sizes + n, 8, hipMemcpyDeviceToHost, xs));
+    BG_HIP(hipStreamSynchronize(xs));
     h->compactExec = h->execCount;
   }
   const size_t need = 32 + n * sizeof(bg_compact_hdr) + h->compactOps;
@@ -2217,8 +2236,8 @@ extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) 
   E.dst = (uint8_t*)dst;
   // plan pairs, then enough workgroups for the caller pairs decided on the host (and the head)
   const unsigned g = (unsigned)E.nplan + (unsigned)((n + 255) / 256) + 1;
-  BG_HIP(hipLaunchKernel(bg_compact_write_kernel_ptr(), dim3(g), dim3(256), args, 0, h->stream));
-  BG_HIP(hipStreamSynchronize(h->stream));
+  BG_HIP(hipLaunchKernel(bg_compact_write_kernel_ptr(), dim3(g), dim3(256), args, 0, xs));
+  BG_HIP(hipStreamSynchronize(xs));
   *bytes = need;
   return BG_OK;
 }

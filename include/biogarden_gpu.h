@@ -267,11 +267,25 @@ int bg_group_align_batch(bg_group* g, int mode, size_t npairs, const uint8_t* co
                          const size_t* n1, const uint8_t* const* s2, const size_t* n2,
                          const bg_scoring* scoring, int32_t a, int32_t b, bg_pair_result* results,
                          uint8_t* out1, uint8_t* out2, size_t out_cap);
+/* The same call in two halves, so that three batches are in flight (SURVEY §8(d)'s wall pipelined):
+ * bg_group_submit splits the batch, moves the group's scratch dims on, and has every member
+ * prepare and execute its shard, then returns; bg_group_collect finishes the OLDEST submitted
+ * batch (the members' compact exports, the gather, the download and the expansion into
+ * results / out1 / out2, out_cap >= that batch's sum(n1 + n2)).  The pair arrays are copied at
+ * submit; the sequence bytes must stay valid until the batch's collect.  At most 3 batches are
+ * submitted and not collected (a fourth submit: BG_E_ARG; a collect with none: BG_E_ARG);
+ * bg_group_align_batch needs none pending.  bg_group_pending: how many are. */
+int bg_group_submit(bg_group* g, int mode, size_t npairs, const uint8_t* const* s1, const size_t* n1,
+                    const uint8_t* const* s2, const size_t* n2, const bg_scoring* scoring, int32_t a,
+                    int32_t b);
+int bg_group_collect(bg_group* g, bg_pair_result* results, uint8_t* out1, uint8_t* out2, size_t out_cap);
+int bg_group_pending(const bg_group* g);
 /* Host-only: the group's split of a batch over nshards (shard_of[p] for every pair). */
 int bg_group_plan(size_t npairs, const size_t* n1, const size_t* n2, int nshards, int32_t* shard_of);
 int bg_group_buffer_size(bg_group* g, size_t* rows, size_t* cols);
-/* Accumulated ms per phase of bg_group_align_batch: [0] prepare + execute, [1] the members'
- * waits and exports, [2] the gather, [3] the download, [4] the expansion; *calls the call count. */
+/* Accumulated ms per phase of bg_group_align_batch / submit / collect: [0] prepare + execute
+ * (submit), [1] the members' waits and exports, [2] the gather, [3] the download, [4] the
+ * expansion; *calls the count of collected batches. */
 int bg_group_timing(bg_group* g, double* ms, size_t n, uint64_t* calls, int reset);
 
 /* Host-side time of this handle's bg_batch_prepare / bg_batch_fetch calls, accumulated (ms):

@@ -86,3 +86,57 @@ def test_group_more_members_than_pairs():
     want, _ = _single("global", [pairs], -11, -1)
     got, _, _ = _group([0, 0, 0, 0, 0], "global", [pairs], -11, -1)
     assert got == want
+
+
+def _decode(pairs, res, o1, o2):
+    b1, b2 = bytes(o1), bytes(o2)
+    out = []
+    for p in range(len(pairs)):
+        r = res[p]
+        lo, hi = r.offset, r.offset + r.len
+        out.append({"status": r.status, "score": r.score, "aligned1": b1[lo:hi], "aligned2": b2[lo:hi],
+                    "end": (r.end_i, r.end_j), "start": (r.start1, r.start2)})
+    return out
+
+
+@pytest.mark.parametrize("rccl_self", ["0", "1"])
+@pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("local", -11, -1)])
+def test_group_pipelined_submit_collect(monkeypatch, rccl_self, mode, a, b):
+    """bg_group_submit / bg_group_collect with three batches in flight: the same results and scratch
+    history as one aligner fed the batches in order; a fourth submit and an empty collect refuse."""
+    from biogarden_amd import _native
+    monkeypatch.setenv("BG_GROUP_RCCL_SELF", rccl_self)
+    rng = random.Random(41 + len(mode))
+    batches = []
+    for t in range(6):
+        pairs = []
+        for k in range(rng.randint(3, 30)):
+            s1 = rand_seq(rng, rng.choice([0, 1, 150, 700, 1023, 1024, 1500, 2600]), DNA)
+            s2 = mutate(rng, s1, DNA, 0.1) if k % 2 else rand_seq(rng, rng.randint(0, 2000), DNA)
+            pairs.append((s1, s2))
+        batches.append(pairs)
+    want, dims = _single(mode, batches, a, b)
+    sc = _native.builtin_scoring(_native.BG_BLOSUM62)
+    g = _native.Group([0, 0])
+    try:
+        got, tickets = [], []
+        for pairs in batches:
+            if len(tickets) == 3:
+                t = tickets.pop(0)
+                got.append(_decode(t[6], *g.collect(t)))
+            tickets.append(g.submit(mode, pairs, sc, a, b))
+            assert g.pending() == len(tickets)
+        with pytest.raises(RuntimeError):
+            g.submit(mode, batches[0], sc, a, b)        # a fourth batch in flight
+        with pytest.raises(RuntimeError):
+            g.align_batch(mode, batches[0], sc, a, b)   # needs none pending
+        while tickets:
+            t = tickets.pop(0)
+            got.append(_decode(t[6], *g.collect(t)))
+        assert g.pending() == 0
+        with pytest.raises(RuntimeError):
+            g.collect((None, None, None, None, 0, 0, []))
+        assert g.buffer_size() == dims
+    finally:
+        g.close()
+    assert got == want
