@@ -183,6 +183,9 @@ extern "C" bg_group* bg_group_new(const int* devices, int n) {
       bg_aligner*& hh = g->h[kGSlots * m + sl];
       hh = (first == m && sl == 0) ? bg_aligner_new(devices[m]) : bg_aligner_new_shared(g->h[kGSlots * first]);
       if (!hh || bg_set_pipeline(hh, 2) != BG_OK) { bg_group_free(g); return nullptr; }
+      // the device's whole stream set now, before RCCL creates streams of its own (see
+      // bg_aligner_aux_stream)
+      if (first == m && sl == 0 && !bg_aligner_aux_stream(hh)) { bg_group_free(g); return nullptr; }
     }
   }
   const int nr = (int)g->rankDev.size();

@@ -513,8 +513,14 @@ extern "C" int bg_last_hip_error(void) { return g_lastHip; }
 // downloads and exports, so the group's gather queues there instead of on a stream of its own (a
 // fifth stream shares a hardware queue with the DP stream at the box's 4 queues, and its copies
 // wait behind the DPs queued there)
+// It also creates the shared upload stream, so that a caller creating other streams afterwards
+// (bg_group: RCCL's communicator) cannot put one of them between the device's DP, traceback,
+// upload and download streams in the round-robin of hardware queues: an upload stream on the
+// traceback's queue queued each batch's upload behind the previous batch's traceback, and so the
+// next DP (measured: DPs 1.5 ms apart, the traceback in between, tools/r05/group_trace.sh).
 extern "C" void* bg_aligner_aux_stream(bg_aligner* h) {
   if (!h || hipSetDevice(h->device) != hipSuccess) return nullptr;
+  if (!h->upS) h->upS = group_stream(h, kSUp);
   if (!h->dlS) h->dlS = group_stream(h, kSDl);
   return (void*)h->dlS;
 }
