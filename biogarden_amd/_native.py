@@ -508,14 +508,18 @@ class Group:
                                     ctypes.byref(scoring), a, b))
         return (a1, n1, a2, n2, total, len(pairs), pairs)
 
-    def collect(self, ticket):
+    def collect(self, ticket, bufs=None):
         """bg_group_collect for the oldest submitted batch (pass its ticket): -> (results, out1,
-        out2) as align_batch_raw."""
+        out2) as align_batch_raw.  bufs: a (results, out1, out2) triple to reuse, as large as the
+        batch needs (a streaming caller rotates a few; fresh buffers fault their pages in)."""
         total, n = ticket[4], ticket[5]
-        res = (BgPairResult * max(n, 1))()
-        o1 = (ctypes.c_uint8 * max(total, 1))()
-        o2 = (ctypes.c_uint8 * max(total, 1))()
-        check(lib().bg_group_collect(self._p, res, o1, o2, total))
+        if bufs is not None and len(bufs[0]) >= n and len(bufs[1]) >= total and len(bufs[2]) >= total:
+            res, o1, o2 = bufs
+        else:
+            res = (BgPairResult * max(n, 1))()
+            o1 = (ctypes.c_uint8 * max(total, 1))()
+            o2 = (ctypes.c_uint8 * max(total, 1))()
+        check(lib().bg_group_collect(self._p, res, o1, o2, max(total, 1) if bufs is None else len(o1)))
         return res, o1, o2
 
     def pending(self):
