@@ -50,7 +50,11 @@ extern "C" void* bg_finish_grp4_kernel_ptr(int R, int mode);
 extern "C" void* bg_finish_grp2_kernel_ptr(int R, int mode);
 extern "C" void* bg_dp_grp_kernel_ptr(int R, int P);
 extern "C" int bg_dp_grp_wave_lds_bytes(int R, int P);
+extern "C" void* bg_dp_grp16_kernel_ptr(int R);
+extern "C" int bg_dp_grp16_wave_lds_bytes(int R);
 // grouped pairs, P per wave (bg_grp_kernel.hip, bg_grp_finish.hip)
+// (P = 8: two pairs per lane in 16-bit halves, bg_grp16_kernel.hip; each half's checkpoints have
+// the four-pair layout, so the traceback is P = 4's)
 static size_t bg_finish_grp_lds_bytes(int P, int R, int nslots, int nw, int* win) {
   return P == 2 ? bg_finish_grp2_lds_bytes(R, nslots, nw, win) : bg_finish_grp4_lds_bytes(R, nslots, nw, win);
 }
@@ -573,7 +577,7 @@ static bool grp_fold(const bg_aligner* h) {
 // more waves (profiles/r05/grouped/pmc_c4_p*.json).  Off when the groups would average under
 // 0.6 P pairs.  BG_GROUPED=0 never, =1 at any fill; BG_GRP_P=2 / 4 forces P.  Returns P, or 0.
 static int plan_grouped(bg_aligner* h, size_t npairs, const size_t* n1, const size_t* n2,
-                        const uint8_t* const* s2, int* Rout, int* Wout, std::vector<int>& refOf) {
+                        const uint8_t* const* s2, int64_t dmax, int* Rout, int* Wout, std::vector<int>& refOf) {
   const char* e = std::getenv("BG_GROUPED");
   if (e && e[0] == '0') return 0;
   const bool force = e && e[0] == '1';
@@ -617,13 +621,41 @@ static int plan_grouped(bg_aligner* h, size_t npairs, const size_t* n1, const si
   }
   size_t g4 = 0, g2 = 0;
   for (size_t c : count) { g4 += (c + 3) / 4; g2 += (c + 1) / 2; }
+  // P = 8 (two pairs per lane in 16-bit halves, bg_grp16_kernel.hip) when every cell's frame value
+  // provably fits int16: M'(i, j) lies between the least border value (a gap-only path from the
+  // border adds 0 in the frame) and the largest plus (max S - 2a) per diagonal step; the margin
+  // covers the cells each lane computes before its column 0
+  bool fits16 = maxn1 <= 160;
+  {
+    const long a = h->a, b = h->b;
+    const bool rowLin = h->mode == BG_GLOBAL || h->mode == BG_FITTING, colLin = h->mode == BG_GLOBAL;
+    auto rowv = [&](long j) -> long { return j == 0 ? 0 : (rowLin ? a + (j - 1) * b : 0) - a * j; };
+    auto colv = [&](long i) -> long { return i == 0 ? 0 : (colLin ? a + (i - 1) * b : 0) - a * i; };
+    for (size_t p = 0; p < npairs && fits16; ++p) {
+      if (refOf[p] < 0) continue;
+      const long N1 = (long)n1[p], N2 = (long)n2[p];
+      const long v[6] = {rowv(0), rowv(1), rowv(N2), colv(0), colv(1), colv(N1)};
+      const long lo = *std::min_element(v, v + 6), hi = *std::max_element(v, v + 6);
+      const long grow = std::max<long>(0, (long)dmax) * std::min(N1, N2);
+      if (hi + grow + 4096 > 32767 || lo - 4096 < -32768) fits16 = false;
+    }
+  }
+  size_t g8 = 0;
+  for (size_t c : count) g8 += (c + 7) / 8;
+  // P = 8 only on request (BG_GRP_P=8): it puts one wave where P = 4 puts two, and one wave per
+  // SIMD leaves the step's dependent chain unhidden (C4's 8 192 pairs: DP 1.55 ms against 1.16);
+  // at 16 384 pairs its DP alone is 5 % faster, but beside the tracebacks the step is 28 % slower
+  // 
   int P = maxn1 <= 160 ? 4 : 2;
-  if (const char* ep = std::getenv("BG_GRP_P")) P = (ep[0] == '4' && maxn1 <= 160) ? 4 : 2;
-  const size_t groups = P == 4 ? g4 : g2;
+  (void)g8;
+  if (const char* ep = std::getenv("BG_GRP_P"))
+    P = (ep[0] == '8' && fits16) ? 8 : (ep[0] == '4' && maxn1 <= 160) ? 4 : (ep[0] == '2' || maxn1 > 160) ? 2 : P;
+  const size_t groups = P == 8 ? g8 : P == 4 ? g4 : g2;
   if (!force && 10 * ndp < 6 * (size_t)P * groups) return 0;
+  const int L = P == 8 ? 16 : 64 / P;                   // lanes per pair
   int R = 10;
   for (int r : {2, 3, 4, 5, 8, 10})
-    if ((size_t)(64 / P) * r >= maxn1) { R = r; break; }
+    if ((size_t)L * r >= maxn1) { R = r; break; }
   int W = 4;
   if (const char* ew = std::getenv("BG_GRP_W")) W = std::min(16, std::max(1, std::atoi(ew)));
   *Rout = R;
@@ -734,7 +766,7 @@ static size_t fin_lds(const bg_aligner* h, int R, size_t np, int* win, int* area
   int nw = 4, ns = 0;
   fin_geom(h, np, &nw, &ns);
   if (h->ack) return bg_finish_ack_lds_bytes(R, h->kdim, h->local, ns, nw, win, area);
-  if (h->ckpt && h->grouped) return bg_finish_grp_lds_bytes(h->grouped, R, ns, nw, win);
+  if (h->ckpt && h->grouped) return bg_finish_grp_lds_bytes(h->grouped == 8 ? 4 : h->grouped, R, ns, nw, win);
   if (h->ckpt) return bg_finish_ck_lds_bytes(R, ns, nw, win);
   *win = bg_finish_window_bytes(R, h->affine, np, h->cus);
   return bg_finish_lds_bytes(*win);
@@ -1015,6 +1047,10 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
         if (v - 3 < -128 || v - 2 > 127) tagOK = false;
       }
   h->tag = tagOK ? 1 : 0;
+  int64_t dmaxS2a = -((int64_t)1 << 40);       // max S - 2a over the batch's codes (grouped DP's int16 bound)
+  for (int q = 0; q < KS; ++q)
+    for (int c = 0; c < KS; ++c)
+      if (present[q] && present[c]) dmaxS2a = std::max<int64_t>(dmaxS2a, (int64_t)S.at(q, c) - 2 * (int64_t)a);
   bool ckLimit = false;   // a pair beyond the checkpoint tracebacks' chunk keys (BG_CK_MAX_*)
 plan_again:
   h->ckpt = (h->tag && h->allowCkpt && !ckLimit) ? 1 : 0;
@@ -1040,7 +1076,7 @@ plan_again:
   h->wide = 0;
   h->grouped = 0;
   std::vector<int> refOf;     // grouped DP: caller pair -> reference class (-1: not grouped)
-  if (h->tag && h->ckpt && !h->finFlags) h->grouped = plan_grouped(h, npairs, n1, n2, s2, &R, &W, refOf);
+  if (h->tag && h->ckpt && !h->finFlags) h->grouped = plan_grouped(h, npairs, n1, n2, s2, dmaxS2a, &R, &W, refOf);
   if (h->grouped) {
   } else if (h->tag && plan_wide(h, n1, n2, npairs, &R, &W)) h->wide = 1;
   else plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
@@ -1058,7 +1094,7 @@ plan_again:
     h->codesOff = 0;
     h->codesInLds = 0;
     h->auxLdsOff = 512;
-    lds = 512 + (size_t)W * bg_dp_grp_wave_lds_bytes(R, h->grouped);
+    lds = 512 + (size_t)W * (h->grouped == 8 ? bg_dp_grp16_wave_lds_bytes(R) : bg_dp_grp_wave_lds_bytes(R, h->grouped));
   } else if (h->tag) {
     // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
     // boundary block, output ring, profile entries, the current chunk's codes and the mailbox
@@ -1263,29 +1299,31 @@ plan_again:
       if ((size_t)rc >= byRef.size()) byRef.resize(rc + 1);
       byRef[rc].push_back((int)q);
     }
-    std::vector<std::array<int32_t, 4>> groups;
+    std::vector<std::array<int32_t, 8>> groups;
     for (const auto& v : byRef)
       for (size_t x = 0; x < v.size(); x += GP) {
-        std::array<int32_t, 4> gq = {-1, -1, -1, -1};
+        std::array<int32_t, 8> gq = {-1, -1, -1, -1, -1, -1, -1, -1};
         for (size_t y = 0; y < (size_t)GP && x + y < v.size(); ++y) gq[y] = v[x + y];
         groups.push_back(gq);
       }
-    std::stable_sort(groups.begin(), groups.end(), [&](const std::array<int32_t, 4>& x, const std::array<int32_t, 4>& y) {
+    std::stable_sort(groups.begin(), groups.end(), [&](const std::array<int32_t, 8>& x, const std::array<int32_t, 8>& y) {
       return (uint64_t)h->plan[x[0]].n1 * h->plan[x[0]].n2 > (uint64_t)h->plan[y[0]].n1 * h->plan[y[0]].n2;
     });
     tro = 0;
     h->grpHost.clear();
     for (const auto& gq : groups) {
       const BgPair& P0 = h->plan[gq[0]];
+      // P = 8: the low halves (y < 4) as a four-pair group at tro, the high ones right after
+      const uint64_t area = (uint64_t)P0.nc * (R + 1) * BG_WAVE * 4;
       for (int y = 0; y < GP; ++y) {
         h->grpHost.push_back(gq[y]);
         if (gq[y] < 0) continue;
         BgPair& P = h->plan[gq[y]];
-        P.trace_off = tro;
-        P.lane0 = (64 / GP) * y;
-        P.lanes = 64 / GP;
+        P.trace_off = tro + (GP == 8 && y >= 4 ? area : 0);
+        P.lane0 = GP == 8 ? 16 * (y & 3) : (64 / GP) * y;
+        P.lanes = GP == 8 ? 16 : 64 / GP;
       }
-      tro += round_up((uint64_t)P0.nc * (R + 1) * BG_WAVE * 4, 256);
+      tro += round_up((GP == 8 ? 2 : 1) * area, 256);
     }
     h->ngroups = (int)groups.size();
   }
@@ -1572,7 +1610,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[0], ds));
   if (np) {
-    void* fn = h->grouped ? bg_dp_grp_kernel_ptr(h->R, h->grouped)
+    void* fn = h->grouped == 8 ? bg_dp_grp16_kernel_ptr(h->R)
+             : h->grouped ? bg_dp_grp_kernel_ptr(h->R, h->grouped)
              : h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : dp_fn(h, h->R);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
@@ -1785,10 +1824,11 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
     } else if (h->ckpt) {
       int win = 0;
-      const size_t lds = h->grouped ? bg_finish_grp_lds_bytes(h->grouped, h->R, fns, fnw, &win)
+      const int fgp = h->grouped == 8 ? 4 : h->grouped;   // P = 8: the halves' layout is P = 4's
+      const size_t lds = h->grouped ? bg_finish_grp_lds_bytes(fgp, h->R, fns, fnw, &win)
                                     : bg_finish_ck_lds_bytes(h->R, fns, fnw, &win);
       F.win_bytes = win;
-      void* ffn = h->grouped ? bg_finish_grp_kernel_ptr(h->grouped, h->R, h->mode) : bg_finish_ck_kernel_ptr(h->R, h->mode);
+      void* ffn = h->grouped ? bg_finish_grp_kernel_ptr(fgp, h->R, h->mode) : bg_finish_ck_kernel_ptr(h->R, h->mode);
       if (lds > 65536) BG_HIP(hipFuncSetAttribute(ffn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       if (!h->split) {
         BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));

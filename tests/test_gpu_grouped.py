@@ -42,14 +42,14 @@ def _key(r):
     return (r.status, r[0], bytes(r[1].chain), bytes(r[2].chain))
 
 
-@pytest.mark.parametrize("P", ["4", "2"])
+@pytest.mark.parametrize("P", ["8", "4", "2"])
 def test_grouped_C4_slice_matches_ungrouped(oracle, P):
     from tools import workloads as w
     pairs = w.c4_pairs(nrefs=8, reads_per_ref=131)          # 131 per reference: partial groups
     res, st = _align("semiglobal", pairs, -1, -2, "", P)
     ng = 8 * ((131 + int(P) - 1) // int(P))
     assert st["grouped"] == ng and st["group_pairs"] == int(P) and st["checkpoint"] == 1, st
-    assert st["R"] == (10 if P == "4" else 5), st
+    assert st["R"] == (5 if P == "2" else 10), st
     assert (st["fin_waves"], st["fin_slots"]) == (1, 6), st
     ref, st0 = _align("semiglobal", pairs, -1, -2, "0")
     assert st0["grouped"] == 0, st0
@@ -62,7 +62,7 @@ def test_grouped_C4_slice_matches_ungrouped(oracle, P):
 
 def _edge_pairs(seed, R, mode, P):
     rng = random.Random(seed)
-    top = (64 // P) * R
+    top = (16 if P == 8 else 64 // P) * R
     reflens = [1, 5, 63, 64, 65, 127, 200, 700]
     if mode == "fitting":                                   # seq2 fits in seq1 (n2 <= n1)
         reflens = [1, 2, 5, max(1, top // 4), max(1, top // 2), top - 1, top]
@@ -85,7 +85,7 @@ def _edge_pairs(seed, R, mode, P):
     return pairs
 
 
-@pytest.mark.parametrize("P", [4, 2])
+@pytest.mark.parametrize("P", [8, 4, 2])
 @pytest.mark.parametrize("R", [2, 3, 5, 8, 10])
 @pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("global", -2, -2), ("fitting", -1, -1),
                                       ("overlap", -1, -3)])
