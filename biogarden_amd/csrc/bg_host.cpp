@@ -374,6 +374,18 @@ extern "C" int bg_abi_version(void) { return BG_ABI_VERSION; }
 static hipStream_t group_stream(bg_aligner* h, int which) {
   StreamGroup& G = *h->sg;
   std::lock_guard<std::mutex> lk(G.mu);
+  // BG_QPRIO (experiment): 1 = the DP streams at the highest queue priority, 2 = the traceback
+  // streams at the lowest, 3 = both (workgroup dispatch order when both kernels wait for room)
+  const char* qp = std::getenv("BG_QPRIO");
+  const int qv = qp ? std::atoi(qp) : 0;
+  int lo = 0, hi = 0;
+  const bool dpS = which == kSDp || which == kSDps, finS = which == kSFin || which == kSFin2 || which == kSFin3;
+  if (!G.s[which] && qv && ((dpS && (qv & 1)) || (finS && (qv & 2))) &&
+      hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+    if (hipStreamCreateWithPriority(&G.s[which], hipStreamNonBlocking, dpS ? hi : lo) != hipSuccess)
+      G.s[which] = nullptr;
+    return G.s[which];
+  }
   if (!G.s[which] && hipStreamCreateWithFlags(&G.s[which], hipStreamNonBlocking) != hipSuccess)
     G.s[which] = nullptr;
   return G.s[which];
