@@ -58,6 +58,8 @@ def main():
     ap.add_argument("--timing", action="store_true", help="finish-kernel cycle breakdown (stderr)")
     ap.add_argument("--rank", type=int, default=0, help="C4 / C5: the shard this GPU runs")
     ap.add_argument("--world", type=int, default=8, help="C4 / C5: GPUs the job is sharded over")
+    ap.add_argument("--warm-ms", type=float, default=0.0,
+                    help="untimed executes for at least this long before the timed ones")
     ap.add_argument("--single", type=int, default=0,
                     help="also time N lone executes (execute + synchronize each): one alignment's wall")
     args = ap.parse_args()
@@ -86,6 +88,11 @@ def main():
         st = h.stats()
         h.execute()
         h.synchronize()
+        tw = time.perf_counter()
+        while (time.perf_counter() - tw) * 1e3 < args.warm_ms:
+            h.execute()
+            h.execute()
+            h.synchronize()
         h.profile_begin()
         t0 = time.perf_counter()
         for _ in range(args.steps):
