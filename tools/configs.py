@@ -58,6 +58,7 @@ def main():
     ap.add_argument("--timing", action="store_true", help="finish-kernel cycle breakdown (stderr)")
     ap.add_argument("--rank", type=int, default=0, help="C4 / C5: the shard this GPU runs")
     ap.add_argument("--world", type=int, default=8, help="C4 / C5: GPUs the job is sharded over")
+    ap.add_argument("--torch-init", action="store_true", help="initialise torch on the GPU first")
     ap.add_argument("--warm-ms", type=float, default=0.0,
                     help="untimed executes for at least this long before the timed ones")
     ap.add_argument("--single", type=int, default=0,
@@ -65,6 +66,10 @@ def main():
     args = ap.parse_args()
     if args.timing:
         os.environ["BG_FINISH_TIMING"] = "1"
+    if args.torch_init:                  # torch's HIP runtime state first, as in bench.py
+        import torch
+        torch.zeros(1, device="cuda")
+        torch.cuda.synchronize()
     from biogarden_amd import _native
     h = _native.Handle(0)
     h.set_pipeline(args.pipeline)
