@@ -454,6 +454,7 @@ def main():
     ap.add_argument("--cpu-one-pairs", type=int, default=8, help="M pairs for the 1-core CPU rate")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-affine", action="store_true")
+    ap.add_argument("--no-steady", action="store_true", help="skip the 200-step steady-state timing")
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--no-h2h", action="store_true", help="skip the host-to-host timing")
     ap.add_argument("--h2h-handles", type=int, default=4,
@@ -542,6 +543,16 @@ def main():
     total_cells = sum_over_ranks(cells)
     gcups = total_cells * args.steps / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
+    # not `value`: the same batch over 200 steps, where the first DP (no traceback beside it) and
+    # the last traceback (nothing beside it) weigh 1/200 instead of 1/K
+    steady = None
+    if not strong_head and not args.no_steady:
+        ks = 200
+        el_s, dp_s, fin_s = timed(h, ks, 2, barrier)
+        el_s = max_over_ranks(el_s)
+        steady = {"steps": ks, "value": round(total_cells * ks / el_s / 1e9, 3),
+                  "ms_per_step": round(el_s / ks * 1e3, 4), "dp_ms": round(dp_s, 4),
+                  "finish_ms": round(fin_s, 4)}
 
     # ---- results: RCCL gather of every rank's packed results to rank 0 (after the timed
     # region for the weak form; the strong form gathered inside every step)
@@ -654,6 +665,7 @@ def main():
                                                  "step" if strong_head
                                                  else "independent pairs per rank")},
         "roofline": roof,
+        "steady_state": steady,
         "cpu_baseline": cpu,
         "affine": aff,
         "strong": strong,
