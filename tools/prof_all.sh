@@ -14,8 +14,8 @@ G1="SQ_WAVES SQ_INSTS_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WA
 METHOD="rocprofv3 --kernel-trace --pmc, one counter group per pass ($G1 | FETCH_SIZE | WRITE_SIZE), pipeline depth 3 as timed; averages over the DP dispatches"
 for leg in ${LEGS:-M MA C2 C3 C4 C5}; do
   case $leg in
-    M)  CMD="bench.py --no-cpu --no-h2h --no-affine --configs= --steps 6 --warmup 2"; WL=semiglobal_256x10000x10000_blosum62_o1_e2 ;;
-    MA) CMD="bench.py --no-cpu --no-h2h --no-affine --configs= --steps 6 --warmup 2 --open -11 --extend -1"; WL=semiglobal_256x10000x10000_blosum62_o11_e1 ;;
+    M)  CMD="bench.py --no-cpu --no-h2h --no-affine --no-steady --configs= --steps 6 --warmup 2"; WL=semiglobal_256x10000x10000_blosum62_o1_e2 ;;
+    MA) CMD="bench.py --no-cpu --no-h2h --no-affine --no-steady --configs= --steps 6 --warmup 2 --open -11 --extend -1"; WL=semiglobal_256x10000x10000_blosum62_o11_e1 ;;
     *)  CMD="tools/configs.py $leg --steps 4"; WL=$leg ;;
   esac
   i=0; mkdir -p $OUT/pmc_$leg
