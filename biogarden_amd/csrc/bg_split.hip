@@ -187,6 +187,9 @@ __device__ void exit_item(const BgSplitArgs& A, int item, int lane, int* wl) {
   const bool capItem = capStrip && ts >= c0 * 64 && ts < c1 * 64;
   uint32_t* done = reinterpret_cast<uint32_t*>(ar + L.done);
   if (!CONC && !capItem && done[(size_t)(s - 1) * L.G + g] == A.epoch) return;   // done beside the DP
+  // the start strip's items after the capture item feed nothing: the strip's bottom row is not
+  // wanted and the chain and resolve stop at the capture segment (head[5])
+  if (capStrip && c0 * 64 > ts) return;
 
   int* prof = wl;                                       // [code][k][lane]
   unsigned* bIn = reinterpret_cast<unsigned*>(wl + 4 * R * 64);
