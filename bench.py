@@ -10,12 +10,17 @@ extend -1, the genuinely affine three-matrix DP and the reference's one-cell-lat
 
 One step = one pass of the hot path over the batch with the inputs resident in HBM: DP kernel
 -> end-cell search -> traceback writing both aligned strings (aligner.rs:351-435), three
-pipeline slots (the traceback of step k overlaps the DP of step k+1).  Every rank aligns its own
-256 pairs (weak scaling: the pairs are independent, no data-path collective); after the timed
-region the per-rank packed results are gathered to rank 0 over RCCL (gather_ms).  With more than
-one rank the line also carries `strong`: ONE batch of 256 pairs LPT-sharded over the ranks, each
-step ending with the device-side export and the RCCL gather to rank 0 inside the timed wall
-(§8(d)'s wall).  `--shard` makes that form the headline.
+pipeline slots (the traceback of step k overlaps the DP of step k+1).
+
+N GPUs ("the same 256 pairs are sharded over G in {1,2,4,8} (strong scaling)"):
+one process per GPU.  `--gpus N` with N > 1 outside torch.distributed starts
+`torch.distributed.run --nproc-per-node N` as a child before anything touches a GPU and exits
+with its code; under torch.distributed the ranks must equal --gpus and (RCCL) each rank needs
+a device of its own, else the bench fails.  The N > 1 headline is the strong form: ONE batch of
+256 pairs LPT-sharded over the ranks, every step = execute + the device-side compact export
+(bg_batch_export_compact_async, no host wait) + the RCCL gather of the records to rank 0,
+pipelined, all inside the timed wall.  `weak` beside it: every rank aligns its own 256 pairs
+(the record gather after the timed region).  `--weak` makes the weak form the headline.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -423,6 +428,130 @@ def config_leg(h, sc, name, barrier, pipeline, steps=None):
         out["value_covers"] = "one alignment: execute + synchronize wall, median of 5 (single)"
     return out
 
+# ------------------------------------------------------------------ N ranks
+
+
+def spawn_ranks(argv, n):
+    """--gpus N > 1 outside torch.distributed: N ranks under torch.distributed.run as a CHILD
+    process, started before this process touches a GPU (no HIP call has run here); returns the
+    child's exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    return subprocess.call(cmd)
+
+
+class StrongGather:
+    """The per-step result path of the strong form, with no host wait: the last
+    execute's compact record goes into a device buffer of its own (bg_batch_export_compact_async,
+    torch's current stream made to wait for it), then one gather of the fixed-capacity records
+    to rank 0 (RCCL send / recv queued on that stream; every rank's capacity is exchanged once).
+    Buffers rotate over `ring` steps; a buffer is reused only after the event recorded behind
+    its gather.  With gloo (the CPU rehearsal) the record is copied to the host first."""
+
+    def __init__(self, h, dist, coll_dev, ring=8):
+        import torch
+        self.h, self.dist, self.coll_dev = h, dist, coll_dev
+        self.cap = h.export_compact_bound()
+        self.caps = [self.cap]
+        if dist is not None:
+            t = torch.tensor([self.cap], dtype=torch.int64, device=coll_dev)
+            caps = [torch.zeros(1, dtype=torch.int64, device=coll_dev) for _ in range(dist.get_world_size())]
+            dist.all_gather(caps, t)
+            self.caps = [int(c.item()) for c in caps]
+        self.rank = 0 if dist is None else dist.get_rank()
+        self.ring = ring
+        self.send = [torch.empty(self.cap, dtype=torch.uint8, device="cuda") for _ in range(ring)]
+        self.recv = None
+        if self.rank == 0 and dist is not None:
+            self.recv = [[torch.empty(c, dtype=torch.uint8, device=coll_dev) for c in self.caps]
+                         for _ in range(ring)]
+        self.done = [None] * ring
+        self.i = 0
+        self.last = None
+
+    def __call__(self):
+        import torch
+        k = self.i % self.ring
+        self.i += 1
+        if self.done[k] is not None:
+            self.done[k].synchronize()
+        buf = self.send[k]
+        stream = torch.cuda.current_stream()
+        self.h.export_compact_async(buf.data_ptr(), self.cap, stream.cuda_stream)
+        dist = self.dist
+        if dist is None:
+            self.last = [buf]
+        else:
+            src = buf if self.coll_dev == "cuda" else buf.cpu()
+            if self.rank == 0:
+                bufs = self.recv[k]
+                ops = [dist.P2POp(dist.irecv, bufs[r], r) for r in range(1, len(bufs))]
+                bufs[0] = src
+            else:
+                ops = [dist.P2POp(dist.isend, src, 0)]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            self.last = bufs if self.rank == 0 else None
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        self.done[k] = ev
+
+    def records(self):
+        """rank 0: the last step's records (bytes, trimmed to their own size), rank order."""
+        import struct
+        if self.last is None:
+            return None
+        out = []
+        for b in self.last:
+            raw = b.cpu().numpy().tobytes()
+            _, n, ops, _ = struct.unpack_from("<4Q", raw, 0)
+            out.append(raw[:32 + 48 * n + ops])
+        return out
+
+
+def dry_line(args, world, rank, dist):
+    """--dry-run (no GPU): the N-rank plumbing alone — the ranks torch.distributed.run started,
+    the LPT shards of one batch, a per-pair record of each rank's shard (index, lengths, CRC32 of
+    both sequences) gathered to rank 0 with the same variable-size gather, merged in caller order
+    and compared with the same records made for the whole batch in one process.  No alignment
+    runs: `value` is null."""
+    import zlib
+
+    import torch
+    from biogarden_amd import shard
+    pairs = make_pairs(args.pairs, args.len1, args.len2, SEED)
+    sizes = [(len(x), len(y)) for x, y in pairs]
+    shards = shard.lpt_shards(sizes, world)
+
+    def rec(p):
+        return (p, len(pairs[p][0]), len(pairs[p][1]), zlib.crc32(pairs[p][0]), zlib.crc32(pairs[p][1]))
+
+    mine = shards[rank]
+    blob = json.dumps([rec(p) for p in mine]).encode()
+    if dist is not None:
+        packed = shard.gather_packed(torch.frombuffer(bytearray(blob), dtype=torch.uint8), dist, dst=0)
+    else:
+        packed = [blob]
+    if rank != 0:
+        return
+    per = [[tuple(r) for r in json.loads(b.decode())] for b in packed]
+    merged = shard.merge_shards(shards, per)
+    single = [rec(p) for p in range(len(pairs))]
+    print(json.dumps({"metric": METRIC, "value": None, "unit": "GCUPS", "dry_run": True,
+                      "ranks": world, "n_gpus": 0, "devices": [], "gpus_arg": args.gpus,
+                      "pairs": len(pairs), "shard_pairs": [len(x) for x in shards],
+                      "shard_cells": [sum(sizes[p][0] * sizes[p][1] for p in x) for x in shards],
+                      "gathered_pairs": sum(len(x) for x in per),
+                      "gather_equals_single": merged == single,
+                      "covers": "torch.distributed.run children, LPT shards, variable-size gather "
+                                "to rank 0, merge in caller order; no GPU work"}))
+
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -442,9 +571,11 @@ def main():
     ap.add_argument("--pipeline", type=int, default=3,
                     help="slots: >= 2 lets the traceback of step k overlap the DP of step k+1 "
                          "(two HIP streams); 3 absorbs traceback times that vary around the DP's")
-    ap.add_argument("--shard", action="store_true",
-                    help="strong scaling as the headline: LPT-shard one batch of --pairs over the "
-                         "ranks, export + gather inside every step")
+    ap.add_argument("--weak", action="store_true",
+                    help="N > 1: the weak form (own --pairs per rank) as the headline instead of "
+                         "the strong form (one batch of --pairs LPT-sharded over the ranks)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: the N-rank plumbing only (spawn, shards, gather, merge), value null")
     ap.add_argument("--config", choices=["C2", "C3", "C4", "C5"],
                     help="headline = this whole SURVEY 8(d) job LPT-sharded over the ranks, "
                          "export + gather to rank 0 inside every step")
@@ -473,23 +604,61 @@ def main():
                          "default 0..N-1")
     args = ap.parse_args()
 
-    import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    # N ranks: one process per GPU.  Outside torch.distributed, --gpus N > 1 starts the N ranks
+    # as a child (before anything here touches a GPU) and exits with its code; inside it, the
+    # ranks must be what --gpus asks for
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None and not args.group:
+        sys.exit(spawn_ranks(sys.argv[1:], args.gpus))
+    world = int(world_env or "1")
+    if world != args.gpus and not args.group:
+        print("bench.py: %d ranks under torch.distributed but --gpus %d" % (world, args.gpus),
+              file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # BG_BENCH_BACKEND=gloo rehearses the N > 1 path on a box with fewer GPUs than ranks (ranks
-    # share devices round-robin, collectives on host tensors); the driver's runs use RCCL
-    backend = os.environ.get("BG_BENCH_BACKEND", "nccl")
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    # BG_BENCH_BACKEND=gloo rehearses the N > 1 path with ranks sharing devices (collectives on
+    # host tensors; the line says how many devices ran); the driver's runs use RCCL, one GPU per rank
+    backend = "gloo" if args.dry_run else os.environ.get("BG_BENCH_BACKEND", "nccl")
     coll_dev = "cuda" if backend == "nccl" else "cpu"
+
+    import torch
+    dist = None
     if world > 1:
         import torch.distributed as dist
-        local_rank = local_rank % max(1, torch.cuda.device_count())
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        dry_line(args, world, rank, dist)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+    ndev = torch.cuda.device_count()          # no HIP initialisation on this image
+    if world > 1:
+        if ndev < 1 or (backend == "nccl" and ndev < local_world):
+            print("bench.py: %d ranks on this node need %d GPUs, %d visible (BG_BENCH_BACKEND=gloo "
+                  "rehearses with ranks sharing devices)" % (local_world, local_world, ndev),
+                  file=sys.stderr)
+            sys.exit(3)
+        local_rank = local_rank % ndev
         torch.cuda.set_device(local_rank)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group(backend)
+    # the devices that ran: (host, PCI bus id) of every rank's GPU
+    props = torch.cuda.get_device_properties(local_rank)
+    me = (os.uname().nodename, "%s:%s" % (getattr(props, "pci_domain_id", 0), getattr(props, "pci_bus_id", local_rank)))
+    if dist is not None:
+        everyone = [None] * world
+        dist.all_gather_object(everyone, me)
+    else:
+        everyone = [me]
+    n_devices = len(set(everyone))
+    if backend == "nccl" and n_devices != world:
+        print("bench.py: %d ranks ran on %d distinct GPUs" % (world, n_devices), file=sys.stderr)
+        sys.exit(3)
 
     from biogarden_amd import _native
 
@@ -522,25 +691,58 @@ def main():
     h.set_pipeline(args.pipeline)
     sc = _native.builtin_scoring(_native.BG_BLOSUM62)
 
+    args.n_devices = n_devices
     if args.config:
         job_line(args, h, sc, world, rank, dist, coll_dev, barrier, max_over_ranks, sum_over_ranks)
         return
 
-    # ---- M: the metric workload (own 256 pairs per rank; --shard: one batch sharded)
-    strong_head = args.shard and world > 1
+    # ---- M: the metric workload.  N = 1: the 256 pairs.  N > 1: the strong form (one batch of
+    # 256 pairs LPT-sharded, export + gather in every step) and the weak form (own 256 per rank)
+    workload = workload_name(args.mode, args.pairs, args.len1, args.len2, args.open, args.extend)
+    own = make_pairs(args.pairs, args.len1, args.len2, SEED + 1000003 * rank)   # rank 0: the batch
+    strong_head = world > 1 and not args.weak
+
+    def weak_leg(hh):
+        hh.prepare(args.mode, own, sc, args.open, args.extend)
+        st_ = hh.stats()
+        el, dp, fin = timed(hh, args.steps, args.warmup, barrier)
+        return st_, max_over_ranks(el), dp, fin, sum_over_ranks(st_["cells"])
+
+    def strong_leg(hh):
+        spairs, sdims, shards = sharded_job(make_pairs(args.pairs, args.len1, args.len2, SEED),
+                                            args.mode, args.open, args.extend, world, rank)
+        hh.set_call_dims(sdims)
+        hh.prepare(args.mode, spairs, sc, args.open, args.extend)
+        st_ = hh.stats()
+        g = None if args.no_gather else StrongGather(hh, dist, coll_dev)
+        el, dp, fin = timed(hh, args.steps, args.warmup, barrier, g)
+        return st_, max_over_ranks(el), dp, fin, sum_over_ranks(st_["cells"]), g, spairs, shards
+
+    gather_ms = None
+    heads0 = None
+    gstats = {}
+    strong = weak = None
+    expand_check = None
     if strong_head:
-        pairs, dims, _ = sharded_job(make_pairs(args.pairs, args.len1, args.len2, SEED), args.mode,
-                                     args.open, args.extend, world, rank)
-        h.set_call_dims(dims)
+        st, elapsed, dp_ms, fin_ms, total_cells, g, pairs, shards = strong_leg(h)
+        if g is not None and rank == 0:
+            recs = g.records()
+            heads0 = [_native.compact_headers(b) for b in recs]
+            # rank 0 expands the last step's gathered records into aligned strings (it holds the
+            # inputs): the merged batch must be complete, in caller order, every status 0
+            batch = make_pairs(args.pairs, args.len1, args.len2, SEED)
+            te = time.perf_counter()
+            per = [_native.expand_compact(rec, [batch[p] for p in idx]) for rec, idx in zip(recs, shards)]
+            from biogarden_amd import shard as _shard
+            merged = _shard.merge_shards(shards, per)
+            expand_check = {"pairs": len(merged), "complete": all(r is not None for r in merged),
+                            "expand_ms": round((time.perf_counter() - te) * 1e3, 2),
+                            "covers": "rank 0, bg_compact_expand of the last step's gathered "
+                                      "records (after the timed steps)"}
     else:
-        pairs = make_pairs(args.pairs, args.len1, args.len2, SEED + 1000003 * rank)
-    h.prepare(args.mode, pairs, sc, args.open, args.extend)
-    st = h.stats()
+        st, elapsed, dp_ms, fin_ms, total_cells = weak_leg(h)
+        pairs = own
     cells = st["cells"]
-    gstep = gatherer(h, dist, coll_dev) if (strong_head and not args.no_gather) else None
-    elapsed, dp_ms, fin_ms = timed(h, args.steps, args.warmup, barrier, gstep)
-    elapsed = max_over_ranks(elapsed)
-    total_cells = sum_over_ranks(cells)
     gcups = total_cells * args.steps / elapsed / 1e9
     ms_per_step = elapsed / args.steps * 1e3
     # not `value`: the same batch over 200 steps, where the first DP (no traceback beside it) and
@@ -553,51 +755,50 @@ def main():
         steady = {"steps": ks, "value": round(total_cells * ks / el_s / 1e9, 3),
                   "ms_per_step": round(el_s / ks * 1e3, 4), "dp_ms": round(dp_s, 4),
                   "finish_ms": round(fin_s, 4)}
-
-    # ---- results: RCCL gather of every rank's packed results to rank 0 (after the timed
-    # region for the weak form; the strong form gathered inside every step)
-    gather_ms = None
-    heads0 = None
-    gstats = {}
-    if dist is not None and not args.no_gather:
-        g = gstep or gatherer(h, dist, coll_dev, gstats)
-        barrier()
-        tg = time.perf_counter()
-        packed = g()
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) * 1e3
-        if rank == 0:
-            heads0 = [_native.compact_headers(b) for b in packed]
-    else:
-        heads0 = [_native.compact_headers(b) for b in gatherer(h, None, coll_dev, gstats)()]
-    workload = workload_name(args.mode, args.pairs, args.len1, args.len2, args.open, args.extend)
     roof = roofline(st, cells, dp_ms, workload, args.open, args.extend, fin_ms)
     roof["finish_ms"] = round(fin_ms, 4)
+    if strong_head:
+        roof["share"] = "rank 0's LPT share: %d of %d pairs" % (len(pairs), args.pairs)
 
-    # ---- strong scaling beside the weak headline (N > 1): one batch of 256 pairs over the ranks
-    strong = None
-    if world > 1 and not args.shard:
+    # ---- the other form beside the headline (N > 1)
+    if world > 1 and strong_head:
+        wst, wel, wdp, wfin, wtotal = weak_leg(h)
+        weak = {"value": round(wtotal * args.steps / wel / 1e9, 3), "unit": "GCUPS",
+                "ms_per_step": round(wel / args.steps * 1e3, 4), "pairs_per_rank": len(own),
+                "dp_ms": round(wdp, 4), "finish_ms": round(wfin, 4), "scaling": "weak",
+                "gather_in_wall": False, "kernel": kernel_info(wst, args.pipeline)}
+    elif world > 1:
         hs = _native.Handle(local_rank)
         hs.set_pipeline(args.pipeline)
-        spairs, sdims, _ = sharded_job(make_pairs(args.pairs, args.len1, args.len2, SEED),
-                                       args.mode, args.open, args.extend, world, rank)
-        hs.set_call_dims(sdims)
-        hs.prepare(args.mode, spairs, sc, args.open, args.extend)
-        sst = hs.stats()
-        se, sdp, sfin = timed(hs, args.steps, args.warmup, barrier, gatherer(hs, dist, coll_dev))
-        se = max_over_ranks(se)
-        scells = sum_over_ranks(sst["cells"])
+        sst, se, sdp, sfin, scells, _, spairs, _ = strong_leg(hs)
         strong = {"value": round(scells * args.steps / se / 1e9, 3), "unit": "GCUPS",
                   "ms_per_step": round(se / args.steps * 1e3, 4), "pairs_total": args.pairs,
                   "pairs_this_rank": len(spairs), "dp_ms": round(sdp, 4), "finish_ms": round(sfin, 4),
-                  "gather_in_wall": True, "scaling": "strong"}
+                  "gather_in_wall": True, "scaling": "strong", "kernel": kernel_info(sst, args.pipeline)}
         hs.close()
+
+    # ---- results of the weak form: RCCL gather of every rank's packed results to rank 0 after
+    # the timed region (the strong form gathered inside every step); N = 1: the export alone
+    if not strong_head:
+        if dist is not None and not args.no_gather:
+            gfun = gatherer(h, dist, coll_dev, gstats)
+            barrier()
+            tg = time.perf_counter()
+            packed = gfun()
+            torch.cuda.synchronize()
+            gather_ms = (time.perf_counter() - tg) * 1e3
+            if rank == 0:
+                heads0 = [_native.compact_headers(b) for b in packed]
+        else:
+            heads0 = [_native.compact_headers(b) for b in gatherer(h, None, coll_dev, gstats)()]
+    if weak is not None and rank == 0:
+        weak["gather_ms"] = gather_ms
 
     # ---- MA: the same pairs with a genuinely affine gap model (open < extend)
     aff = None
     if not args.no_affine:
         a2, b2 = args.affine_open, args.affine_extend
-        h.prepare(args.mode, pairs, sc, a2, b2)
+        h.prepare(args.mode, own, sc, a2, b2)
         sta = h.stats()
         na = max(2, args.steps // 2)
         ea, dpa, fina = timed(h, na, max(1, args.warmup // 2), barrier)
@@ -622,7 +823,7 @@ def main():
     h2h = None
     if not args.no_h2h:
         queues = int(os.environ.get("GPU_MAX_HW_QUEUES") or 4)
-        h2h = host_to_host(pairs, args.mode, args.open, args.extend, local_rank,
+        h2h = host_to_host(own, args.mode, args.open, args.extend, local_rank,
                            handles=args.h2h_handles, rounds=args.h2h_rounds,
                            shared=not args.h2h_unshared)
         h2h["hw_queues"] = queues
@@ -634,20 +835,23 @@ def main():
             dist.destroy_process_group()
         return
 
-    ok_status = all(st == 0 for rr in heads0 for st, _, _ in rr)
-    gpu_scores = [sc for _, sc, _ in heads0[0]]
+    ok_status = heads0 is not None and all(x == 0 for rr in heads0 for x, _, _ in rr)
+    if expand_check is not None:
+        ok_status = ok_status and expand_check["complete"]
+    gpu_scores = [x for _, x, _ in heads0[0]] if heads0 else []
 
     # ---- CPU baseline: the oracle on a bounded sample of the same workload (rank 0, N = 1)
     cpu = None
     if not args.no_cpu and world == 1:
-        cpu = cpu_section(pairs, gpu_scores, args.mode, args.open, args.extend, host_info(),
+        cpu = cpu_section(own, gpu_scores, args.mode, args.open, args.extend, host_info(),
                           args.cpu_pairs, args.cpu_one_pairs)
 
     line = {
         "metric": METRIC,
         "value": round(gcups, 3),
         "unit": "GCUPS",
-        "n_gpus": world,
+        "n_gpus": n_devices,
+        "ranks": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
@@ -657,18 +861,24 @@ def main():
         "dtype": "int32",
         "data": "synthetic (uniform DNA, numpy PCG64 seed 0x%X%s)" % (
             SEED, "" if strong_head else " + 1000003*rank"),
-        "config": {"workload": workload, "pairs_per_gpu": len(pairs), "len1": args.len1,
+        "config": {"workload": workload, "pairs_total": args.pairs if strong_head else args.pairs * world,
+                   "pairs_this_rank": len(pairs), "len1": args.len1,
                    "len2": args.len2, "mode": args.mode, "scoring": "blosum62",
                    "gap_open": args.open, "gap_extend": args.extend,
                    "kernel": kernel_info(st, args.pipeline),
-                   "parallelism": "dp%d (%s)" % (world, "one batch LPT-sharded, gather in every "
+                   "parallelism": "dp%d (%s)" % (world, "one batch LPT-sharded over the ranks, "
+                                                 "compact export + RCCL gather to rank 0 in every "
                                                  "step" if strong_head
                                                  else "independent pairs per rank")},
+        "devices": sorted(set("%s/%s" % d for d in everyone)),
+        "collectives": backend if world > 1 else None,
         "roofline": roof,
         "steady_state": steady,
         "cpu_baseline": cpu,
         "affine": aff,
         "strong": strong,
+        "weak": weak,
+        "gathered_expand": expand_check,
         "configs": cfgs,
         "gather_ms": None if gather_ms is None else round(gather_ms, 3),
         "gather_record_bytes_per_rank": gstats.get("record_bytes"),
@@ -721,13 +931,16 @@ def group_line(args):
         g.timing(reset=True)
         t0 = time.perf_counter()
         tickets = []
+        bad = 0                      # pairs of any collected batch with a status other than 0
         for s in range(args.steps):
             if len(tickets) == 3:
                 res, _, _ = g.collect(tickets.pop(0), bufs[(s - 3) % 3])
+                bad += sum(1 for p in range(len(pairs)) if res[p].status != 0)
             tickets.append(g.submit(args.mode, pairs, sc, args.open, args.extend))
         s = args.steps
         while tickets:
             res, _, _ = g.collect(tickets.pop(0), bufs[(s - len(tickets) - 1) % 3])
+            bad += sum(1 for p in range(len(pairs)) if res[p].status != 0)
         el = time.perf_counter() - t0
         ph = g.timing()
     finally:
@@ -751,7 +964,7 @@ def group_line(args):
                                       % (len(devs), devs[0])},
             "host_ms_per_step": {k: round(v / calls, 4) for k, v in ph.items()},
             "survey_8d_wall": True,
-            "all_status_ok": all(res[p].status == 0 for p in range(len(pairs)))}
+            "all_status_ok": bad == 0, "status_checked": "every collected batch"}
     print(json.dumps(line))
 
 
@@ -786,7 +999,8 @@ def job_line(args, h, sc, world, rank, dist, coll_dev, barrier, max_over_ranks, 
         expand_ms = (time.perf_counter() - te) * 1e3
         merged = shard.merge_shards(shards, per)
         line = {"metric": "GCUPS (billion DP cells/s), %s, %d MI355X" % (name, world),
-                "value": round(total * steps / el / 1e9, 3), "unit": "GCUPS", "n_gpus": world,
+                "value": round(total * steps / el / 1e9, 3), "unit": "GCUPS",
+                "n_gpus": args.n_devices, "ranks": world,
                 "steps": steps, "warmup": args.warmup, "ms_per_step": round(el / steps * 1e3, 4),
                 "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                 "dtype": "int32", "data": "synthetic (tools/workloads.py, seed 0xB10A11F0 + %s)" % name[1:],

@@ -28,7 +28,14 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
            "bg_fasta_close", "bg_split_stats", "bg_split_conc_diag", "bg_aligner_new_shared",
            "bg_set_async_fetch", "bg_group_new", "bg_group_free", "bg_group_size",
            "bg_group_member", "bg_group_align_batch", "bg_group_plan", "bg_group_buffer_size",
-           "bg_group_timing", "bg_group_submit", "bg_group_collect", "bg_group_pending"]
+           "bg_group_timing", "bg_group_submit", "bg_group_collect", "bg_group_pending",
+           "bg_get_stats_sized", "bg_batch_export_compact_bound", "bg_batch_export_compact_async",
+           "bg_set_option", "bg_get_option", "bg_wait_diag"]
+
+# bg_set_option keys (include/biogarden_gpu.h BG_OPT_*), by their BG_OPTIONS names
+OPTIONS = ("grouped", "group_pairs", "group_waves", "wide_waves", "fin_waves", "fin_slots",
+           "fin_sync", "fin_selfserve", "split", "split_segment", "split_concurrent",
+           "split_wait_ms", "two_dp_streams", "wait_ms")
 
 
 class NativeUnavailable(RuntimeError):
@@ -122,6 +129,7 @@ def lib():
     L.bg_batch_fetch.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgPairResult), c_u8p, c_u8p,
                                  ctypes.c_size_t]
     L.bg_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats)]
+    L.bg_get_stats_sized.argtypes = [ctypes.c_void_p, ctypes.POINTER(BgStats), ctypes.c_size_t]
     L.bg_split_stats.argtypes = [ctypes.c_void_p] + [ctypes.POINTER(ctypes.c_uint64)] * 5
     L.bg_split_conc_diag.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32)]
     L.bg_aligner_buffer_size.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
@@ -133,6 +141,9 @@ def lib():
     L.bg_set_tuning.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     L.bg_set_pipeline.argtypes = [ctypes.c_void_p, ctypes.c_int]
     L.bg_set_kernel_options.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.bg_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    L.bg_get_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.bg_wait_diag.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), ctypes.c_size_t]
     L.bg_status_string.argtypes = [ctypes.c_int]
     L.bg_status_string.restype = ctypes.c_char_p
     L.bg_abi_version.restype = ctypes.c_int
@@ -141,6 +152,9 @@ def lib():
                                  ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_int)]
     L.bg_batch_export_compact.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.POINTER(ctypes.c_size_t)]
+    L.bg_batch_export_compact_bound.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t)]
+    L.bg_batch_export_compact_async.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                                ctypes.c_void_p]
     L.bg_compact_expand.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t,
                                     ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
                                     ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_size_t),
@@ -235,6 +249,31 @@ class Handle:
         check(lib().bg_set_kernel_options(self._p, (1 if allow_tagged else 0) |
                                           (2 if (allow_tagged and checkpoint) else 0) |
                                           (4 if affine_checkpoint else 0)))
+
+    def set_option(self, name, value):
+        """bg_set_option by name (OPTIONS); value None or -1 restores the automatic choice."""
+        check(lib().bg_set_option(self._p, OPTIONS.index(name), -1 if value is None else int(value)))
+
+    def get_option(self, name):
+        v = ctypes.c_int()
+        check(lib().bg_get_option(self._p, OPTIONS.index(name), ctypes.byref(v)))
+        return v.value
+
+    def options(self, **kw):
+        """Context manager: set options for a block, restore the previous values after it."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            old = {k: self.get_option(k) for k in kw}
+            try:
+                for k, v in kw.items():
+                    self.set_option(k, v)
+                yield self
+            finally:
+                for k, v in old.items():
+                    self.set_option(k, v)
+        return cm()
 
     def set_pipeline(self, depth):
         check(lib().bg_set_pipeline(self._p, depth))
@@ -380,6 +419,19 @@ class Handle:
         check(lib().bg_batch_export_compact(self._p, ctypes.c_void_p(device_ptr), ctypes.byref(n)))
         return n.value
 
+    def export_compact_bound(self):
+        """The compact record's largest size for the prepared batch (no device work)."""
+        n = ctypes.c_size_t(0)
+        check(lib().bg_batch_export_compact_bound(self._p, ctypes.byref(n)))
+        return n.value
+
+    def export_compact_async(self, device_ptr, cap, after_stream=None):
+        """bg_batch_export_compact_async: the last execute's compact record into device memory
+        without a host wait; after_stream (a raw hipStream_t, e.g. torch's current stream's
+        cuda_stream) waits for it."""
+        check(lib().bg_batch_export_compact_async(self._p, ctypes.c_void_p(device_ptr), cap,
+                                                  ctypes.c_void_p(after_stream or 0)))
+
     def edit_distance_batch(self, pairs):
         """analysis::seq::edit_distance over pairs [(s1, s2)] -> [int]."""
         a1, n1, a2, n2, _ = self._arrays(pairs)
@@ -432,7 +484,7 @@ class Handle:
 
     def stats(self):
         st = BgStats()
-        check(lib().bg_get_stats(self._p, ctypes.byref(st)))
+        check(lib().bg_get_stats_sized(self._p, ctypes.byref(st), ctypes.sizeof(st)))
         return {f: getattr(st, f) for f, _ in BgStats._fields_}
 
     def split_stats(self):
@@ -442,6 +494,19 @@ class Handle:
         check(lib().bg_split_stats(self._p, *[ctypes.byref(x) for x in v]))
         return dict(zip(("pairs_split", "strips_taken", "tail_moves", "pairs_overflow", "items_beside_dp"),
                         (x.value for x in v)))
+
+    WAIT_KINDS = {0: None, 1: "walker waited for a chunk", 2: "walker waited for the slot lock",
+                  3: "helper waited for the slot lock", 4: "walker recomputed one chunk over and over"}
+
+    def wait_diag(self):
+        """bg_wait_diag: the last execute's traceback wait that ran out (None if none did)."""
+        v = (ctypes.c_uint32 * 18)()
+        check(lib().bg_wait_diag(self._p, v, 18))
+        if v[0] == 0:
+            return None
+        return {"kind": self.WAIT_KINDS.get(v[0], v[0]), "pair": v[1], "wave": v[2],
+                "key": (v[3] >> 16, v[3] & 0xFFFF), "map": v[4], "filling": v[5], "lock": v[6],
+                "walker": (v[7], v[8]), "recomputed": v[9], "slots": list(v[10:18])}
 
     def conc_diag(self):
         """bg_split_conc_diag: the concurrent exit pass's abandon record (all zero: it ran to
@@ -466,6 +531,7 @@ class Group:
             raise NativeUnavailable("bg_group_new(%r) failed (no such device, or no librccl)"
                                     % (list(devices),))
         self.devices = list(devices)
+        self._tickets = []          # submitted, not yet collected (bg_group_collect takes the oldest)
 
     def close(self):
         if getattr(self, "_p", None):
@@ -506,12 +572,18 @@ class Group:
         a1, n1, a2, n2, total = Handle._arrays(pairs)
         check(lib().bg_group_submit(self._p, MODES.get(mode, mode), len(pairs), a1, n1, a2, n2,
                                     ctypes.byref(scoring), a, b))
-        return (a1, n1, a2, n2, total, len(pairs), pairs)
+        ticket = (a1, n1, a2, n2, total, len(pairs), pairs)
+        self._tickets.append(ticket)
+        return ticket
 
     def collect(self, ticket, bufs=None):
         """bg_group_collect for the oldest submitted batch (pass its ticket): -> (results, out1,
         out2) as align_batch_raw.  bufs: a (results, out1, out2) triple to reuse, as large as the
         batch needs (a streaming caller rotates a few; fresh buffers fault their pages in)."""
+        # bg_group_collect always finishes the OLDEST batch and writes that batch's pair count of
+        # results: any other ticket would size the buffers for the wrong batch
+        if not self._tickets or ticket is not self._tickets[0]:
+            raise ValueError("collect() takes the oldest submitted ticket (submission order)")
         total, n = ticket[4], ticket[5]
         if bufs is not None and len(bufs[0]) >= n and len(bufs[1]) >= total and len(bufs[2]) >= total:
             res, o1, o2 = bufs
@@ -520,6 +592,7 @@ class Group:
             o1 = (ctypes.c_uint8 * max(total, 1))()
             o2 = (ctypes.c_uint8 * max(total, 1))()
         check(lib().bg_group_collect(self._p, res, o1, o2, max(total, 1) if bufs is None else len(o1)))
+        self._tickets.pop(0)
         return res, o1, o2
 
     def pending(self):

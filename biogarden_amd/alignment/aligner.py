@@ -62,6 +62,13 @@ class SequenceAligner:
     def set_tuning(self, R=0, waves=0):
         self._h.set_tuning(R, waves)
 
+    def set_option(self, name, value):
+        """bg_set_option (planner / traceback choices, never results): see _native.OPTIONS."""
+        self._h.set_option(name, value)
+
+    def options(self, **kw):
+        return self._h.options(**kw)
+
     # ---------------------------------------------------------------- batch (Tile) form
     def align_batch(self, mode, pairs, score, a, b, strict=False):
         """Aligns many (seq1, seq2) pairs with one call.  Returns AlignmentResult per pair;

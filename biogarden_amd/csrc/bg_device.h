@@ -203,8 +203,6 @@ struct BgDpArgs {
   unsigned long long* gran;  // tagged WIDE checkpoint mode: strip-boundary rows as {value, epoch}
                              // granules, indexed like bndM (zeroed when allocated)
   uint32_t epoch;          // this execute's granule tag (never 0, never reused by the handle)
-  int32_t wide_pace;       // WIDE: s_sleep(1)s strip 0 adds per 32 steps (slack for the chain)
-  int32_t prio;            // A/B (BG_DP_PRIO=1): the DP's waves issue at s_setprio 1
   // split traceback with the exit pass running beside the DP (bg_split.hip): the slot's split
   // arena (segment-start checkpoints as {value, epoch} granules, every strip's output row as
   // granules too), the exit pass's segment length, and the resident-workgroup counter
@@ -266,7 +264,26 @@ struct BgFinishArgs {
   // grouped single-strip pairs (bg_grp_kernel.hip): chunks are recomputed as 16-lane jobs, up to
   // four per pass, into 16-lane slots
   int32_t grouped;
+  // every spin of the asynchronous traceback on another wave (the walker waiting for a chunk, the
+  // LDS slot lock, a helper waiting for the walker) is bounded by waitTicks of s_memrealtime
+  // (100 MHz); past it the pair ends with BG_INTERNAL and the first such wait writes wdiag
+  // (words below, bg_wait_diag)
+  int32_t waitTicks;
+  uint32_t* wdiag;
 };
+
+// bg_wait_diag's record: the first bounded wait of an execute's traceback that ran out
+enum {
+  BG_WD_NONE = 0,
+  BG_WD_CHUNK = 1,        // the walker waited for a recomputed chunk
+  BG_WD_LOCK_WALKER = 2,  // the walker waited for the slot lock
+  BG_WD_LOCK_HELPER = 3,  // a helper waited for the slot lock
+  BG_WD_THRASH = 4,       // the walker recomputed the same chunk again and again without finding it
+  BG_WD_WORDS = 18
+};
+// words: [0] kind, [1] pair (plan index), [2] wave, [3] key (strip << 16 | chunk), [4] its map
+// entry, [5] slot filling flags (bit z), [6] lock word, [7] walker row, [8] walker column,
+// [9] the walker's recomputations of the key, [10..17] slot keys
 
 // BgFinishArgs::phase
 enum {
@@ -283,7 +300,7 @@ enum {
   BG_FIN_SYNC = 8,         // linear checkpoint traceback: recompute at barriers (BG_FIN_SYNC=1, A/B)
   BG_FIN_SELFSERVE = 16,   // asynchronous traceback: the walker recomputes every miss itself at
                            // once (tests the forward-progress path; BG_FIN_SELFSERVE=1)
-  BG_FIN_NOPRIO = 32,      // the walker keeps priority 0 (A/B of its s_setprio 3; BG_FIN_NOPRIO=1)
+  BG_FIN_NOPRIO = 32,      // the walker keeps priority 0 (many-pair linear batches)
   BG_FIN_DEFER_EXPAND = 64 // split TAIL: the core's op packing and expansion are left to
                            // bg_expand_count_kernel / bg_expand_kernel (many workgroups per pair)
 };

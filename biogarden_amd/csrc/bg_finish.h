@@ -270,6 +270,36 @@ constexpr int kSpecDepth = BG_SPEC_DEPTH;
 constexpr int kSelfPolls = 4096;
 __device__ __forceinline__ int ck_map_idx(int s, int c) { return ((s & 15) << 4) | (c & 15); }
 
+// Bounded waits of the asynchronous traceback (BgFinishArgs::waitTicks, s_memrealtime at 100 MHz)
+__device__ __forceinline__ bool wait_expired(const BgFinishArgs& F, unsigned long long t0) {
+  return (long long)(__builtin_amdgcn_s_memrealtime() - t0) > (long long)F.waitTicks;
+}
+// The first wait of an execute that ran out writes where it stood (one lane; include/
+// biogarden_gpu.h bg_wait_diag): the kind, the pair, the wave, the awaited key, its map entry,
+// the slots' filling flags and keys, the lock word, the walker's cell and its recomputations
+__device__ __noinline__ void wait_diag(const BgFinishArgs& F, int kind, int pidx, int wave, int key,
+                                       const unsigned* ckMap, int* sh, int nSlots, int k, int l,
+                                       int selfN) {
+  if (!F.wdiag) return;
+  if (atomicCAS(F.wdiag, 0u, (unsigned)kind) != 0u) return;
+  uint32_t* d = F.wdiag;
+  d[1] = (uint32_t)pidx;
+  d[2] = (uint32_t)wave;
+  d[3] = (uint32_t)key;
+  d[4] = key >= 0 ? ckMap[ck_map_idx(key >> 16, key & 0xffff)] : 0xFFFFFFFFu;
+  unsigned fl = 0;
+  for (int z = 0; z < nSlots && z < 8; ++z) {
+    if (__hip_atomic_load(&sh[48 + z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) fl |= 1u << z;
+    d[10 + z] = (uint32_t)sh[40 + z];
+  }
+  d[5] = fl;
+  d[6] = (uint32_t)__hip_atomic_load(&sh[36], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  d[7] = (uint32_t)k;
+  d[8] = (uint32_t)l;
+  d[9] = (uint32_t)selfN;
+  __threadfence();
+}
+
 // this wave-lane's profile entries for strip s, built by the whole workgroup
 template <int R>
 __device__ void build_prof_aff(const BgFinishArgs& F, const BgPair& P, int s, int* profTab, int tid, int NT) {
@@ -885,10 +915,24 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     int idle = 0;
     for (;;) {
       if (__hip_atomic_load(&sh[32], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-      int key = -1, zz = -1;
+      int key = -1, zz = -1, lockLost = 0;
       if (lane == 0) {
-        while (__hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+        // the lock is held for a slot scan only; past the wait bound this helper stops helping
+        // (the walker serves itself) and the diag names the holder's state
+        const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+        for (int sp = 1; __hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0; ++sp) {
           help_pause(1);
+          if ((sp & 255) == 0 && wait_expired(F, tl0)) { lockLost = 1; break; }
+        }
+      }
+      if (uni(__shfl(lockLost, 0, 64))) {
+        if (lane == 0)
+          wait_diag(F, BG_WD_LOCK_HELPER, P.index, wid, -1, ckMap, sh, nSlots,
+                    __hip_atomic_load(&sh[34], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
+                    __hip_atomic_load(&sh[35], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
+        break;
+      }
+      if (lane == 0) {
         const int req = __hip_atomic_load(&sh[33], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int kw = __hip_atomic_load(&sh[34], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int lw = __hip_atomic_load(&sh[35], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1162,8 +1206,9 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             // chunk itself.  A chunk already being filled is only waited for (its filler always
             // finishes); the bound below is a last-resort guard that no schedule reaches.
             const int selfPolls = (F.flags & BG_FIN_SELFSERVE) ? 0 : kSelfPolls;
-            int it = 0;
+            int it = 0, selfN = 0, why = BG_WD_CHUNK;
             bool got = false;
+            const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
             for (;; ++it) {
               const unsigned e = __hip_atomic_load(me, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
               if (e != 0xFFFFFFFFu && (int)(e >> 4) == key) {
@@ -1174,10 +1219,16 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                 break;
               }
               if (it >= selfPolls && (it - selfPolls) % 64 == 0) {
-                int zz = -1;
+                int zz = -1, lockLost = 0;
                 if (lane == 0) {
-                  while (__hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+                  const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
+                  for (int sp = 1; __hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0; ++sp) {
                     __builtin_amdgcn_s_sleep(1);
+                    if ((sp & 255) == 0 && wait_expired(F, tl0)) { lockLost = 1; break; }
+                  }
+                }
+                if (uni(__shfl(lockLost, 0, 64))) { why = BG_WD_LOCK_WALKER; break; }
+                if (lane == 0) {
                   // in flight (flags first), then published meanwhile (the map second): see the
                   // helpers' candidate check
                   bool busy = false;
@@ -1232,6 +1283,13 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                          P.nstrips, P.nc, nSlots);
 #endif
                 if (zz >= 0) {
+                  // a chunk the walker recomputed and published is guarded from every eviction
+                  // until the walker reads it: needing it again and again is a defect, not a wait
+                  if (++selfN > 16) {
+                    if (lane == 0) __hip_atomic_store(&sh[48 + zz], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    why = BG_WD_THRASH;
+                    break;
+                  }
                   recompute_chunk<R>(F, P, reqS, reqB0, win + (size_t)zz * kSlotDw, ckArea, lane);
                   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
                   if (lane == 0) {
@@ -1244,10 +1302,16 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                   continue;                                // re-check the map
                 }
               }
-              if (it > (1 << 26)) break;
+              if ((it & 63) == 63 && wait_expired(F, tw)) break;
               __builtin_amdgcn_s_sleep(1);
             }
-            if (!got) { status = 5; done = 1; break; }     // 5: BG_INTERNAL (unreachable)
+            if (!got) {
+              // 5: BG_INTERNAL (no schedule reaches it), with the wait's record in bg_wait_diag
+              if (lane == 0) wait_diag(F, why, P.index, 0, key, ckMap, sh, nSlots, k, l, selfN);
+              status = 5;
+              done = 1;
+              break;
+            }
             k0 = -1000000;                                 // decode the neighbourhood again
             ++nMiss;
             if (F.dbg) tMiss += __builtin_readcyclecounter() - tw0;

@@ -137,7 +137,6 @@ __global__ __launch_bounds__(1024) void bg_dp_grp_kernel(BgDpArgs A) {
   const int g = lane / L, sl = lane % L;
   const int wv = blockIdx.x * W + w;                          // the wave's group of GP pairs
   if (wv >= A.ngroups) return;
-  if (A.prio) __builtin_amdgcn_s_setprio(1);
   const int* grp = A.grp + GP * wv;
   const int p0 = grp[0];                                      // every group has its first pair
   const int pl = grp[g] >= 0 ? grp[g] : p0;                   // this lane's pair

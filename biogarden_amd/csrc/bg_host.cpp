@@ -18,6 +18,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <string>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -50,11 +51,7 @@ extern "C" void* bg_finish_grp4_kernel_ptr(int R, int mode);
 extern "C" void* bg_finish_grp2_kernel_ptr(int R, int mode);
 extern "C" void* bg_dp_grp_kernel_ptr(int R, int P);
 extern "C" int bg_dp_grp_wave_lds_bytes(int R, int P);
-extern "C" void* bg_dp_grp16_kernel_ptr(int R);
-extern "C" int bg_dp_grp16_wave_lds_bytes(int R);
 // grouped pairs, P per wave (bg_grp_kernel.hip, bg_grp_finish.hip)
-// (P = 8: two pairs per lane in 16-bit halves, bg_grp16_kernel.hip; each half's checkpoints have
-// the four-pair layout, so the traceback is P = 4's)
 static size_t bg_finish_grp_lds_bytes(int P, int R, int nslots, int nw, int* win) {
   return P == 2 ? bg_finish_grp2_lds_bytes(R, nslots, nw, win) : bg_finish_grp4_lds_bytes(R, nslots, nw, win);
 }
@@ -141,18 +138,50 @@ struct PinBuf {
 inline size_t round_up(size_t x, size_t m) { return (x + m - 1) / m * m; }
 
 // bg_download_kernel's grid: enough 256-thread blocks to keep PCIe busy, few enough to sit
-// beside the next DP (no LDS, a handful of VGPRs); BG_DL_BLOCKS overrides
-static const unsigned kDownloadBlocks = [] {
-  const char* e = std::getenv("BG_DL_BLOCKS");
-  return e ? (unsigned)std::max(1, std::atoi(e)) : 64u;
-}();
+// beside the next DP (no LDS, a handful of VGPRs)
+static constexpr unsigned kDownloadBlocks = 64u;
+
+// Diagnostics on stderr, chosen once per process by BG_DEBUG (comma-separated): prepare (host
+// phases per prepare / fetch), exec (host time of each execute's steps), dp (WIDE strip timeline
+// of the first pair), finish (traceback phase cycles), plan (the geometry candidates).  They
+// never change results.
+struct BgDebug {
+  bool prepare = false, exec = false, dp = false, finish = false, plan = false;
+};
+static const BgDebug& dbg_flags() {
+  static const BgDebug d = [] {
+    BgDebug x;
+    const char* e = std::getenv("BG_DEBUG");
+    if (!e) return x;
+    std::string v(e);
+    auto has = [&](const char* k) {
+      const size_t n = std::strlen(k);
+      for (size_t at = v.find(k); at != std::string::npos; at = v.find(k, at + 1))
+        if ((at == 0 || v[at - 1] == ',') && (at + n == v.size() || v[at + n] == ',')) return true;
+      return false;
+    };
+    x.prepare = has("prepare");
+    x.exec = has("exec");
+    x.dp = has("dp");
+    x.finish = has("finish");
+    x.plan = has("plan");
+    return x;
+  }();
+  return d;
+}
+
+// bg_set_option names, for BG_OPTIONS ("name=value,...")
+static const char* const kOptNames[BG_OPT_COUNT] = {
+    "grouped", "group_pairs", "group_waves", "wide_waves", "fin_waves", "fin_slots", "fin_sync",
+    "fin_selfserve", "split", "split_segment", "split_concurrent", "split_wait_ms",
+    "two_dp_streams", "wait_ms"};
 
 // Host-side phases of prepare / fetch, accumulated per handle (bg_host_timing) and, with
 // BG_PREPARE_TIMING set, printed per call on stderr
 enum { kPhSync, kPhStage, kPhPlan, kPhAlloc, kPhUpload, kPhFetchWait, kPhFetchCopy, kPhFetchUnpack, kPhN };
 struct PhaseTimer {
   double* acc;
-  bool on = std::getenv("BG_PREPARE_TIMING") != nullptr;
+  bool on = dbg_flags().prepare;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
   char buf[512];
   int n = 0;
@@ -175,10 +204,14 @@ struct PhaseTimer {
 struct Slot {
   DevBuf trace, bndM, bndX, aux, out1, out2, results, ops, gran, split, gprog;
   DevBuf keys;                      // split pairs: bg_endkey_kernel's end-cell keys (2 u64 per pair)
+  DevBuf wdiag;                     // the traceback's bounded-wait record (bg_wait_diag)
   DevBuf xcnt;                      // split pairs: the deferred expansion's per-block counts
   hipEvent_t dpDone = nullptr, finDone = nullptr;
   hipEvent_t resetDone = nullptr;   // the DP's progress words zeroed (the concurrent exit pass waits)
-  bool inflight = false;
+  // a reader of the slot's results queued on another stream (the asynchronous download or
+  // compact export): the next execute into this slot waits for it before its kernels write
+  hipEvent_t readDone = nullptr;
+  bool inflight = false, readPending = false;
 };
 
 // The HIP streams of one handle, or of several handles on one device that share them
@@ -296,6 +329,8 @@ struct bg_aligner {
   uint64_t opsBytes = 0;           // packed core ops per slot (sum of ceil((n1+n2)/4))
   uint64_t cells = 0, traceBytes = 0, bndBytes = 0, resBytes = 0, outBytes = 0;
   int tuneR = 0, tuneW = 0;
+  int opt[BG_OPT_COUNT];            // bg_set_option, -1 = automatic
+  int o(int key, int dflt) const { return opt[key] < 0 ? dflt : opt[key]; }
   float dp_ms = 0.f, fin_ms = 0.f;
   hipEvent_t last[4] = {nullptr, nullptr, nullptr, nullptr};
 
@@ -374,18 +409,6 @@ extern "C" int bg_abi_version(void) { return BG_ABI_VERSION; }
 static hipStream_t group_stream(bg_aligner* h, int which) {
   StreamGroup& G = *h->sg;
   std::lock_guard<std::mutex> lk(G.mu);
-  // BG_QPRIO (experiment): 1 = the DP streams at the highest queue priority, 2 = the traceback
-  // streams at the lowest, 3 = both (workgroup dispatch order when both kernels wait for room)
-  const char* qp = std::getenv("BG_QPRIO");
-  const int qv = qp ? std::atoi(qp) : 0;
-  int lo = 0, hi = 0;
-  const bool dpS = which == kSDp || which == kSDps, finS = which == kSFin || which == kSFin2 || which == kSFin3;
-  if (!G.s[which] && qv && ((dpS && (qv & 1)) || (finS && (qv & 2))) &&
-      hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
-    if (hipStreamCreateWithPriority(&G.s[which], hipStreamNonBlocking, dpS ? hi : lo) != hipSuccess)
-      G.s[which] = nullptr;
-    return G.s[which];
-  }
   if (!G.s[which] && hipStreamCreateWithFlags(&G.s[which], hipStreamNonBlocking) != hipSuccess)
     G.s[which] = nullptr;
   return G.s[which];
@@ -402,8 +425,10 @@ static hipError_t drain(bg_aligner* h) {
       if (s && (e = hipStreamSynchronize(s)) != hipSuccess) return e;
     return hipSuccess;
   }
-  for (const Slot& S : h->slot)
+  for (const Slot& S : h->slot) {
     if (S.inflight && (e = hipEventSynchronize(S.finDone)) != hipSuccess) return e;
+    if (S.readPending && (e = hipEventSynchronize(S.readDone)) != hipSuccess) return e;
+  }
   if (h->dlExec >= 0 && (e = hipEventSynchronize(h->dlDone)) != hipSuccess) return e;
   if (h->upPending && (e = hipEventSynchronize(h->upDone)) != hipSuccess) return e;
   return hipSuccess;
@@ -415,6 +440,22 @@ static bg_aligner* aligner_init(int device, const std::shared_ptr<StreamGroup>& 
   if (hipSetDevice(device) != hipSuccess) return nullptr;
   bg_aligner* h = new bg_aligner();
   h->device = device;
+  for (int& v : h->opt) v = -1;
+  if (const char* e = std::getenv("BG_OPTIONS")) {
+    // "name=value,...": the tools' way to set bg_set_option (read once, here)
+    std::string all(e);
+    for (size_t at = 0; at <= all.size();) {
+      size_t end = all.find(',', at);
+      if (end == std::string::npos) end = all.size();
+      const std::string kv = all.substr(at, end - at);
+      const size_t eq = kv.find('=');
+      if (eq != std::string::npos)
+        for (int k = 0; k < BG_OPT_COUNT; ++k)
+          if (kv.compare(0, eq, kOptNames[k]) == 0 && std::strlen(kOptNames[k]) == eq)
+            h->opt[k] = std::atoi(kv.c_str() + eq + 1);
+      at = end + 1;
+    }
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     h->cus = prop.multiProcessorCount;
@@ -439,7 +480,8 @@ static bg_aligner* aligner_init(int device, const std::shared_ptr<StreamGroup>& 
   }
   for (Slot& S : h->slot)
     if (hipEventCreateWithFlags(&S.dpDone, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&S.finDone, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&S.finDone, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&S.readDone, hipEventDisableTiming) != hipSuccess) {
       bg_aligner_free(h);
       return nullptr;
     }
@@ -465,9 +507,11 @@ extern "C" void bg_aligner_free(bg_aligner* h) {
     for (DevBuf* d : {&S.trace, &S.bndM, &S.bndX, &S.aux, &S.out1, &S.out2, &S.results, &S.ops, &S.gran, &S.split,
                       &S.gprog, &S.keys, &S.xcnt})
       d->release();
+    S.wdiag.release();
     if (S.dpDone) (void)hipEventDestroy(S.dpDone);
     if (S.finDone) (void)hipEventDestroy(S.finDone);
     if (S.resetDone) (void)hipEventDestroy(S.resetDone);
+    if (S.readDone) (void)hipEventDestroy(S.readDone);
   }
   for (auto& e : h->ev)
     if (e) (void)hipEventDestroy(e);
@@ -484,6 +528,18 @@ extern "C" int bg_set_tuning(bg_aligner* h, int R, int waves) {
     return BG_E_ARG;
   h->tuneR = R;
   h->tuneW = waves;
+  return BG_OK;
+}
+
+extern "C" int bg_set_option(bg_aligner* h, int key, int value) {
+  if (!h || key < 0 || key >= BG_OPT_COUNT || value < -1) return BG_E_ARG;
+  h->opt[key] = value;
+  return BG_OK;
+}
+
+extern "C" int bg_get_option(bg_aligner* h, int key, int* value) {
+  if (!h || !value || key < 0 || key >= BG_OPT_COUNT) return BG_E_ARG;
+  *value = h->opt[key];
   return BG_OK;
 }
 
@@ -573,10 +629,9 @@ static int pipeline_phases(int S, int gw, int NC, int lag = 2) {
 // and every caught-up consumer adds its hand-off latency to the pace of the strips below it.
 // Fitted on C3's DP at R = 2 / 4 / 5 / 8 (12.3 / 10.1 / 9.8 / 10.3 ms): R = 5.
 // grouped semiglobal / overlap batches: the DP folds each pair's last-row end-cell key, so the
-// traceback's one wave does not fold 10 k-column rows (BG_GRP_FOLD=0: the finish folds them)
+// traceback's one wave does not fold 10 k-column rows
 static bool grp_fold(const bg_aligner* h) {
-  static const bool off = [] { const char* e = std::getenv("BG_GRP_FOLD"); return e && e[0] == '0'; }();
-  return h->grouped && !off && (h->mode == BG_SEMIGLOBAL || h->mode == BG_OVERLAP);
+  return h->grouped && (h->mode == BG_SEMIGLOBAL || h->mode == BG_OVERLAP);
 }
 
 // Grouped planner (bg_grp_kernel.hip): every computed pair's read at most 320
@@ -587,12 +642,13 @@ static bool grp_fold(const bg_aligner* h) {
 // 2 048 waves, 513 M VALU instructions) against 1.34 ms at P = 2 (R = 5, 4 096 waves, 674 M) —
 // the DP is VALU-bound (72 % of the SIMDs' quad-cycle issue), so fewer instructions per cell beat
 // more waves (profiles/r05/grouped/pmc_c4_p*.json).  Off when the groups would average under
-// 0.6 P pairs.  BG_GROUPED=0 never, =1 at any fill; BG_GRP_P=2 / 4 forces P.  Returns P, or 0.
+// 0.6 P pairs.  BG_OPT_GROUPED 0 never, 1 at any fill; BG_OPT_GROUP_PAIRS 2 / 4 forces P.
+// Returns P, or 0.
 static int plan_grouped(bg_aligner* h, size_t npairs, const size_t* n1, const size_t* n2,
                         const uint8_t* const* s2, int64_t dmax, int* Rout, int* Wout, std::vector<int>& refOf) {
-  const char* e = std::getenv("BG_GROUPED");
-  if (e && e[0] == '0') return 0;
-  const bool force = e && e[0] == '1';
+  const int og = h->o(BG_OPT_GROUPED, -1);
+  if (og == 0) return 0;
+  const bool force = og == 1;
   size_t maxn1 = 0, ndp = 0;
   for (size_t p = 0; p < npairs; ++p) {
     if (h->prestatus[p] >= 0 || n1[p] == 0 || n2[p] == 0) continue;
@@ -633,43 +689,17 @@ static int plan_grouped(bg_aligner* h, size_t npairs, const size_t* n1, const si
   }
   size_t g4 = 0, g2 = 0;
   for (size_t c : count) { g4 += (c + 3) / 4; g2 += (c + 1) / 2; }
-  // P = 8 (two pairs per lane in 16-bit halves, bg_grp16_kernel.hip) when every cell's frame value
-  // provably fits int16: M'(i, j) lies between the least border value (a gap-only path from the
-  // border adds 0 in the frame) and the largest plus (max S - 2a) per diagonal step; the margin
-  // covers the cells each lane computes before its column 0
-  bool fits16 = maxn1 <= 160;
-  {
-    const long a = h->a, b = h->b;
-    const bool rowLin = h->mode == BG_GLOBAL || h->mode == BG_FITTING, colLin = h->mode == BG_GLOBAL;
-    auto rowv = [&](long j) -> long { return j == 0 ? 0 : (rowLin ? a + (j - 1) * b : 0) - a * j; };
-    auto colv = [&](long i) -> long { return i == 0 ? 0 : (colLin ? a + (i - 1) * b : 0) - a * i; };
-    for (size_t p = 0; p < npairs && fits16; ++p) {
-      if (refOf[p] < 0) continue;
-      const long N1 = (long)n1[p], N2 = (long)n2[p];
-      const long v[6] = {rowv(0), rowv(1), rowv(N2), colv(0), colv(1), colv(N1)};
-      const long lo = *std::min_element(v, v + 6), hi = *std::max_element(v, v + 6);
-      const long grow = std::max<long>(0, (long)dmax) * std::min(N1, N2);
-      if (hi + grow + 4096 > 32767 || lo - 4096 < -32768) fits16 = false;
-    }
-  }
-  size_t g8 = 0;
-  for (size_t c : count) g8 += (c + 7) / 8;
-  // P = 8 only on request (BG_GRP_P=8): it puts one wave where P = 4 puts two, and one wave per
-  // SIMD leaves the step's dependent chain unhidden (C4's 8 192 pairs: DP 1.55 ms against 1.16);
-  // at 16 384 pairs its DP alone is 5 % faster, but beside the tracebacks the step is 28 % slower
-  // 
   int P = maxn1 <= 160 ? 4 : 2;
-  (void)g8;
-  if (const char* ep = std::getenv("BG_GRP_P"))
-    P = (ep[0] == '8' && fits16) ? 8 : (ep[0] == '4' && maxn1 <= 160) ? 4 : (ep[0] == '2' || maxn1 > 160) ? 2 : P;
-  const size_t groups = P == 8 ? g8 : P == 4 ? g4 : g2;
+  const int op = h->o(BG_OPT_GROUP_PAIRS, 0);
+  if (op == 2 || (op == 4 && maxn1 <= 160)) P = op;
+  (void)dmax;
+  const size_t groups = P == 4 ? g4 : g2;
   if (!force && 10 * ndp < 6 * (size_t)P * groups) return 0;
-  const int L = P == 8 ? 16 : 64 / P;                   // lanes per pair
+  const int L = 64 / P;                                 // lanes per pair
   int R = 10;
   for (int r : {2, 3, 4, 5, 8, 10})
     if ((size_t)L * r >= maxn1) { R = r; break; }
-  int W = 4;
-  if (const char* ew = std::getenv("BG_GRP_W")) W = std::min(16, std::max(1, std::atoi(ew)));
+  const int W = std::min(16, std::max(1, h->o(BG_OPT_GROUP_WAVES, 4)));
   *Rout = R;
   *Wout = W;
   h->tagRow = 0;
@@ -689,9 +719,8 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
   size_t maxn1 = 0;
   for (size_t p : comp) maxn1 = std::max(maxn1, n1[p]);
   if (maxn1 < 64 * 4 * 16) return false;                   // one workgroup's 16 waves suffice
-  int W = 4;
   // (the WIDE kernel is built for at most 4 waves per workgroup, bg_tag_kernel.hip)
-  if (const char* e = std::getenv("BG_WIDE_W")) W = std::max(1, std::min(4, std::atoi(e)));
+  const int W = std::max(1, std::min(4, h->o(BG_OPT_WIDE_WAVES, 4)));
   const int cand[] = {2, 3, 4, 5, 8, 10};
   double best = 1e300;
   int bestR = 0;
@@ -748,7 +777,7 @@ static void* fin_fn(const bg_aligner* h, int R) {
 // Finish workgroup of the checkpoint modes: waves (the walker + recompute helpers) and
 // recomputed-chunk slots.  Few pairs: 4 waves and every slot (the walk's latency is the step's
 // tail).  Many pairs: fewer waves and slots, so more pairs walk per CU at once (the walks are
-// latency-bound).  BG_FIN_WAVES / BG_FIN_SLOTS override (experiments).
+// latency-bound).  BG_OPT_FIN_WAVES / BG_OPT_FIN_SLOTS override.
 static void fin_geom(const bg_aligner* h, size_t np, int* nw, int* nslots) {
   *nw = 4;
   *nslots = 0;
@@ -761,13 +790,11 @@ static void fin_geom(const bg_aligner* h, size_t np, int* nw, int* nslots) {
   // shape 1 548 -> 1 656 / 1 767 -> 1 854 GCUPS at 1 024 / 4 096 pairs; the C5 shape, global
   // protein, loses with it: 2 576 -> 2 490)
   if (h->ack && h->local && np > (size_t)h->cus * 2) { *nw = 1; *nslots = 2; }
-  if (const char* e = std::getenv("BG_FIN_WAVES")) *nw = std::min(4, std::max(1, std::atoi(e)));
-  if (const char* e = std::getenv("BG_FIN_SLOTS")) *nslots = std::max(0, std::atoi(e));
   // grouped pairs: the walker recomputes up to four 16-lane chunks in one pass itself (one wave)
   // into small slots (bg_finish.h recompute_grp)
   if (h->grouped) { *nw = 1; *nslots = 6; }
-  if (const char* e = std::getenv("BG_FIN_WAVES")) *nw = std::min(4, std::max(1, std::atoi(e)));
-  if (const char* e = std::getenv("BG_FIN_SLOTS")) *nslots = std::max(0, std::atoi(e));
+  if (h->opt[BG_OPT_FIN_WAVES] >= 0) *nw = std::min(4, std::max(1, h->opt[BG_OPT_FIN_WAVES]));
+  if (h->opt[BG_OPT_FIN_SLOTS] >= 0) *nslots = h->opt[BG_OPT_FIN_SLOTS];
   if (*nslots && *nslots < *nw + 1) *nslots = *nw + 1;
   if (h->grouped && *nslots && *nslots < 4) *nslots = 4;
 }
@@ -778,7 +805,7 @@ static size_t fin_lds(const bg_aligner* h, int R, size_t np, int* win, int* area
   int nw = 4, ns = 0;
   fin_geom(h, np, &nw, &ns);
   if (h->ack) return bg_finish_ack_lds_bytes(R, h->kdim, h->local, ns, nw, win, area);
-  if (h->ckpt && h->grouped) return bg_finish_grp_lds_bytes(h->grouped == 8 ? 4 : h->grouped, R, ns, nw, win);
+  if (h->ckpt && h->grouped) return bg_finish_grp_lds_bytes(h->grouped, R, ns, nw, win);
   if (h->ckpt) return bg_finish_ck_lds_bytes(R, ns, nw, win);
   *win = bg_finish_window_bytes(R, h->affine, np, h->cus);
   return bg_finish_lds_bytes(*win);
@@ -918,7 +945,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
   // per SIMD, then the estimate
   const Cand* pick = nullptr;
   const bool manyAckPlan = h->ack && !h->tuneW && np >= 2 * (size_t)h->cus;
-  if (std::getenv("BG_PLAN_DEBUG"))
+  if (dbg_flags().plan)
     for (const Cand& c : cands)
       std::fprintf(stderr, "plan R %d W %d wps %d T %.4g\n", c.R, c.W, c.wps, c.T);
   // (the affine / local checkpoint path pays taller strips again in the traceback's
@@ -967,7 +994,7 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   ++h->nPrepare;
   BG_HIP(drain(h));
   tm.mark(kPhSync, "sync");
-  for (Slot& S : h->slot) S.inflight = false;
+  for (Slot& S : h->slot) S.inflight = S.readPending = false;
   h->dlExec = -1;
   h->execCount = 0;
   h->prepared = false;
@@ -1106,7 +1133,7 @@ plan_again:
     h->codesOff = 0;
     h->codesInLds = 0;
     h->auxLdsOff = 512;
-    lds = 512 + (size_t)W * (h->grouped == 8 ? bg_dp_grp16_wave_lds_bytes(R) : bg_dp_grp_wave_lds_bytes(R, h->grouped));
+    lds = 512 + (size_t)W * bg_dp_grp_wave_lds_bytes(R, h->grouped);
   } else if (h->tag) {
     // tagged kernel (bg_tag_kernel.hip): 16 produced + 16 consumed counters, then per wave the
     // boundary block, output ring, profile entries, the current chunk's codes and the mailbox
@@ -1214,16 +1241,15 @@ plan_again:
       // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8
       // share one, MI355X_MICROARCH.md), so consecutive indices in the group (consecutive strips:
       // a boundary row handed through HBM) go to blocks of one XCD class, and the hand-offs stay
-      // inside one XCD's L2 except at the seven class boundaries.  BG_WIDE_LINEAR: plain order.
+      // inside one XCD's L2 except at the seven class boundaries.
       const int b0 = (int)h->wgmap.size(), G = P.wg_count;
-      const bool linear = std::getenv("BG_WIDE_LINEAR") != nullptr;
       int cls[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int g = 0; g < G; ++g) ++cls[(b0 + g) & 7];
       int first[8], seen[8] = {0, 0, 0, 0, 0, 0, 0, 0};
       for (int x = 0, acc = 0; x < 8; ++x) { first[(b0 + x) & 7] = acc; acc += cls[(b0 + x) & 7]; }
       for (int g = 0; g < G; ++g) {
         const int x = (b0 + g) & 7;
-        h->wgmap.push_back(make_int2((int)h->plan.size(), linear ? g : first[x] + seen[x]++));
+        h->wgmap.push_back(make_int2((int)h->plan.size(), first[x] + seen[x]++));
       }
       h->progWords += (uint32_t)(P.wg_count * W);
     }
@@ -1238,10 +1264,8 @@ plan_again:
   h->splitItems = h->splitResolve = 0;
   h->splitInts = 0;
   {
-    const char* ev = std::getenv("BG_SPLIT");
-    const char* es = std::getenv("BG_SPLIT_SEGC");
-    h->segc = es ? std::max(1, std::atoi(es)) : BG_SPLIT_SEGC;
-    bool ok = h->wide && h->ckpt && !h->affine && !h->finFlags && mode != BG_LOCAL && !(ev && ev[0] == '0');
+    h->segc = std::max(1, h->o(BG_OPT_SPLIT_SEGMENT, BG_SPLIT_SEGC));
+    bool ok = h->wide && h->ckpt && !h->affine && !h->finFlags && mode != BG_LOCAL && h->o(BG_OPT_SPLIT, -1) != 0;
     bool multi = false;
     for (const BgPair& P : h->plan) {
       if (P.n2 + 1 >= BG_SPLIT_SYM(R)) ok = false;
@@ -1283,8 +1307,8 @@ plan_again:
       // the concurrent pass takes items in the order the DP makes them ready: strip s reaches
       // chunk c at about (3 s + c) chunk times (a strip starts ~3 chunks after the one above)
       {
-        const char* ec = std::getenv("BG_SPLIT_CONC");
-        h->splitConc = !ec ? 2 : ec[0] == '1' ? 1 : 0;
+        const int oc = h->o(BG_OPT_SPLIT_CONCURRENT, -1);
+        h->splitConc = oc < 0 ? 2 : oc == 1 ? 1 : 0;
       }
       std::vector<std::pair<int64_t, int32_t>> keyed;
       keyed.reserve(h->splitItems);
@@ -1563,12 +1587,12 @@ struct CallClock {
 }  // namespace
 
 extern "C" int bg_batch_execute(bg_aligner* h) {
-  static const bool callTiming = std::getenv("BG_EXEC_TIMING") != nullptr;
+  const bool callTiming = dbg_flags().exec;
   CallClock clk("execute", callTiming);
   if (!h) return BG_E_ARG;
   if (!h->prepared) return BG_E_NO_BATCH;
-  // BG_EXEC_TIMING: host time of this call's steps on stderr (which HIP call blocks)
-  static const bool exTiming = std::getenv("BG_EXEC_TIMING") != nullptr;
+  // BG_DEBUG=exec: host time of this call's steps on stderr (which HIP call blocks)
+  const bool exTiming = dbg_flags().exec;
   auto exT = std::chrono::steady_clock::now();
   char exBuf[256];
   int exN = 0;
@@ -1585,13 +1609,12 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   const int z = h->execCount % h->depth;
   Slot& S = h->slot[z];
   // the DP's stream: WIDE batches alternate two (see bg_aligner::dps)
-  // (C3, pipeline 3: 8.35 -> 4.82 ms per execute; BG_TWO_DP_STREAMS=0 keeps one).  Two WIDE DPs
+  // (C3, pipeline 3: 8.35 -> 4.82 ms per execute; BG_OPT_TWO_DP_STREAMS 0 keeps one).  Two WIDE DPs
   // need 2 x gridWgs <= CU count workgroups resident (their strips spin on each other), and
   // nothing else running waits for a DP, so they cannot hold each other's CUs.
   hipStream_t ds = h->stream;
-  const char* e2 = std::getenv("BG_TWO_DP_STREAMS");
-  if (h->wide && h->depth >= 2 && (h->execCount & 1) && !(e2 && e2[0] == '0') && 2 * h->gridWgs <= h->cus &&
-      !std::getenv("BG_DP_TIMING")) {
+  if (h->wide && h->depth >= 2 && (h->execCount & 1) && h->o(BG_OPT_TWO_DP_STREAMS, 1) != 0 &&
+      2 * h->gridWgs <= h->cus && !dbg_flags().dp) {
     if (!h->dps) h->dps = group_stream(h, kSDps);
     if (h->dps) ds = h->dps;
   }
@@ -1610,8 +1633,11 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     }
   }
   if (h->cus - h->gridWgs <= 0) conc = false;
-  // the previous user of this slot must have finished reading its trace
+  // the previous user of this slot must have finished reading its trace, and a download or
+  // export queued behind it reading its results
   if (S.inflight) BG_HIP(hipStreamWaitEvent(ds, S.finDone, 0));
+  if (S.readPending) BG_HIP(hipStreamWaitEvent(ds, S.readDone, 0));
+  S.readPending = false;
   // a shared handle's upload, not waited for by prepare
   if (h->upPending) BG_HIP(hipStreamWaitEvent(ds, h->upDone, 0));
   exMark("waits");
@@ -1622,8 +1648,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   }
   BG_HIP(hipEventRecord(e[0], ds));
   if (np) {
-    void* fn = h->grouped == 8 ? bg_dp_grp16_kernel_ptr(h->R)
-             : h->grouped ? bg_dp_grp_kernel_ptr(h->R, h->grouped)
+    void* fn = h->grouped ? bg_dp_grp_kernel_ptr(h->R, h->grouped)
              : h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : dp_fn(h, h->R);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
@@ -1640,7 +1665,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.wgmap = h->wgmapBuf.as<int2>();
     A.gprog = h->wide ? S.gprog.as<uint32_t>() : h->gprogBuf.as<uint32_t>();
     A.dbg = nullptr;
-    if (std::getenv("BG_DP_TIMING") && h->tag && h->dpDbg.ensure(64 * 4096)) {
+    if (dbg_flags().dp && h->tag && h->dpDbg.ensure(64 * 4096)) {
       A.dbg = h->dpDbg.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, ds));
     }
@@ -1652,11 +1677,6 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.prof_scratch = h->pglob ? h->profScratch.as<int32_t>() : nullptr;
     if (++h->epoch == 0) h->epoch = 1;
     A.epoch = h->epoch;
-    {
-      const char* ev = std::getenv("BG_WIDE_PACE");
-      A.wide_pace = ev ? std::atoi(ev) : 0;
-      A.prio = std::getenv("BG_DP_PRIO") ? 1 : 0;
-    }
     A.gran = S.gran.as<unsigned long long>();
     A.split = conc ? S.split.as<int32_t>() : nullptr;
     A.segc = h->segc;
@@ -1694,8 +1714,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   // At pipeline depth 4 a WIDE batch's tracebacks rotate over three streams: a C3 walk (one
   // latency-bound workgroup, ~13 ms) then hides behind three DPs instead of two.
   int nfs = 1;
-  if ((h->wide || std::getenv("BG_TWO_FIN_STREAMS")) && !std::getenv("BG_FINISH_TIMING") &&
-      !std::getenv("BG_ONE_FIN_STREAM"))
+  if (h->wide && !dbg_flags().finish)
     nfs = h->wide ? std::min(3, std::max(2, h->depth - 1)) : 2;
   // the third stream is created on first use: HIP maps a process's streams onto 4 hardware
   // queues round-robin, and an extra stream per handle moves other handles' copies behind
@@ -1742,8 +1761,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     X.xblocks = h->splitXBlocks;
     X.diag = S.gprog.as<uint32_t>() + h->progWords + 2;
     {
-      const char* ew = std::getenv("BG_SPLIT_WAIT_MS");
-      const long ms = ew ? std::atol(ew) : 500;
+      const long ms = h->o(BG_OPT_SPLIT_WAIT_MS, 500);
       X.waitTicks = (int32_t)std::min<long>(std::max<long>(ms, 1) * 100000L, 0x7FFFFFFFL);
     }
     if (conc && h->splitItems > 0) {
@@ -1795,25 +1813,22 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     F.grouped = h->grouped;
     F.phase = BG_PH_FULL;
     F.segc = h->segc;
-    {
-      static const int2 spec = [] {
-        int d = 2, r = 128;
-        if (const char* e = std::getenv("BG_SPEC")) std::sscanf(e, "%d,%d", &d, &r);
-        return make_int2(std::min(std::max(d, 0), 2), std::max(r, 0));
-      }();
-      F.specDepth = spec.x;
-      F.specAbove = spec.y;
-    }
+    F.specDepth = 2;
+    F.specAbove = 128;
+    if (!S.wdiag.ensure(4 * BG_WD_WORDS)) return BG_E_NOMEM;
+    BG_HIP(hipMemsetAsync(S.wdiag.p, 0, 4 * BG_WD_WORDS, fs));
+    F.wdiag = S.wdiag.as<uint32_t>();
+    F.waitTicks = (int32_t)std::min<long>(std::max<long>(h->o(BG_OPT_WAIT_MS, 2000), 1) * 100000L, 0x7FFFFFFFL);
     F.split = S.split.as<int32_t>();
     F.splitMap = h->splitMapBuf.as<int2>();
-    if (std::getenv("BG_FIN_SYNC")) F.flags |= BG_FIN_SYNC;
-    if (std::getenv("BG_FIN_SELFSERVE")) F.flags |= BG_FIN_SELFSERVE;
+    if (h->o(BG_OPT_FIN_SYNC, 0) == 1) F.flags |= BG_FIN_SYNC;
+    if (h->o(BG_OPT_FIN_SELFSERVE, 0) == 1) F.flags |= BG_FIN_SELFSERVE;
     // the walker's priority 3 costs a many-pair linear batch's DP (the metric: 10 390 -> 10 530
     // GCUPS without it, tools/r04/prio_ab.sh); a WIDE batch's walks are its latency, and the
     // affine walks (recomputing with barriers) gain from it: MA 4 587 -> 4 714 GCUPS, C5 +0.9 %,
-    // C2 even (tools/r05/prio_ab.sh).  BG_FIN_PRIO=1 / BG_FIN_NOPRIO=1 force either.
-    if (std::getenv("BG_FIN_NOPRIO") || (!h->wide && !h->ack && !std::getenv("BG_FIN_PRIO"))) F.flags |= BG_FIN_NOPRIO;
-    if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.ensure(128 * (np + 1))) {
+    // C2 even (tools/r05/prio_ab.sh).
+    if (!h->wide && !h->ack) F.flags |= BG_FIN_NOPRIO;
+    if (dbg_flags().finish && h->dbgBuf.ensure(128 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 128 * np, fs));
     }
@@ -1836,7 +1851,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
     } else if (h->ckpt) {
       int win = 0;
-      const int fgp = h->grouped == 8 ? 4 : h->grouped;   // P = 8: the halves' layout is P = 4's
+      const int fgp = h->grouped;
       const size_t lds = h->grouped ? bg_finish_grp_lds_bytes(fgp, h->R, fns, fnw, &win)
                                     : bg_finish_ck_lds_bytes(h->R, fns, fnw, &win);
       F.win_bytes = win;
@@ -1864,8 +1879,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
         BG_HIP(hipLaunchKernel(ffn, dim3((unsigned)h->splitMap.size()), dim3(64 * fnw), args, lds, fs));
         F.phase = BG_PH_TAIL;
         // the core's packing and expansion by many workgroups per pair (bg_split.hip)
-        const bool defer = !std::getenv("BG_NO_DEFER_EXPAND");
-        if (defer) F.flags |= BG_FIN_DEFER_EXPAND;
+        const bool defer = true;
+        F.flags |= BG_FIN_DEFER_EXPAND;
         BG_HIP(hipLaunchKernel(ffn, dim3(np), dim3(64 * fnw), args, lds, fs));
         if (defer) {
           F.flags &= ~BG_FIN_DEFER_EXPAND;
@@ -1900,7 +1915,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     exMark("dl-wait");
     // the download as a kernel writing the host-mapped buffers (bg_io.hip): the copy-engine form
     // (BG_DL_COPY=1) can block this call for several ms in PyTorch's HIP runtime
-    static const bool dlCopy = std::getenv("BG_DL_COPY") != nullptr;
+    const bool dlCopy = false;
     void* dres = h->hresPin.device_ptr();
     void* d1 = h->ho1.device_ptr();
     void* d2 = h->ho2.device_ptr();
@@ -1923,6 +1938,8 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
       }
     }
     BG_HIP(hipEventRecord(h->dlDone, h->dlS));
+    BG_HIP(hipEventRecord(S.readDone, h->dlS));
+    S.readPending = true;
     h->dlExec = h->execCount;
     exMark("download");
   }
@@ -1959,7 +1976,7 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
   if (rc) return rc;
   tm.mark(kPhFetchWait, "fetch-wait");
   const size_t np = h->plan.size();
-  if (std::getenv("BG_DP_TIMING") && h->dpDbg.p && np) {
+  if (dbg_flags().dp && h->dpDbg.p && np) {
     // first pair's waves: strip start / chunk-0 end / strip end relative to the earliest start
     // (s_memrealtime, 100 MHz, one clock for every XCD), and the shader cycles each wave spent
     // polling for the strip above out of its whole strip (s_memtime)
@@ -1980,7 +1997,7 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
                    (double)d[8 * g + 6], (double)d[8 * g + 7]);
     }
   }
-  if (std::getenv("BG_FINISH_TIMING") && h->dbgBuf.p && np) {
+  if (dbg_flags().finish && h->dbgBuf.p && np) {
     std::vector<unsigned long long> d(16 * np);
     BG_HIP(hipMemcpy(d.data(), h->dbgBuf.p, 128 * np, hipMemcpyDeviceToHost));
     double s[11] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -2119,6 +2136,29 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->split = h->split;
   o->grouped = h->grouped ? h->ngroups : 0;
   o->group_pairs = h->grouped;
+  return BG_OK;
+}
+
+extern "C" int bg_get_stats_sized(bg_aligner* h, bg_stats* o, size_t size) {
+  if (!h || !o) return BG_E_ARG;
+  bg_stats full;
+  const int rc = bg_get_stats(h, &full);
+  if (rc) return rc;
+  std::memcpy(o, &full, std::min(size, sizeof(full)));
+  return BG_OK;
+}
+
+extern "C" int bg_wait_diag(bg_aligner* h, uint32_t* out, size_t n) {
+  if (!h || (!out && n)) return BG_E_ARG;
+  for (size_t x = 0; x < n; ++x) out[x] = 0;
+  if (!h->executed) return BG_OK;
+  const int rc = bg_synchronize(h);
+  if (rc) return rc;
+  const Slot& S = h->slot[h->lastSlot];
+  if (!S.wdiag.p) return BG_OK;
+  uint32_t w[BG_WD_WORDS];
+  BG_HIP(hipMemcpy(w, S.wdiag.p, sizeof(w), hipMemcpyDeviceToHost));
+  for (size_t x = 0; x < n && x < (size_t)BG_WD_WORDS; ++x) out[x] = w[x];
   return BG_OK;
 }
 
@@ -2297,6 +2337,56 @@ extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) 
   BG_HIP(hipLaunchKernel(bg_compact_write_kernel_ptr(), dim3(g), dim3(256), args, 0, xs));
   BG_HIP(hipStreamSynchronize(xs));
   *bytes = need;
+  return BG_OK;
+}
+
+// Upper bound of the compact record of the prepared batch: the header, every caller pair's
+// bg_compact_hdr and every planned pair's packed ops at their largest, ceil((n1 + n2) / 4).
+extern "C" int bg_batch_export_compact_bound(bg_aligner* h, size_t* bytes) {
+  if (!h || !bytes) return BG_E_ARG;
+  if (!h->prepared) return BG_E_NO_BATCH;
+  *bytes = 32 + h->npairs * sizeof(bg_compact_hdr) + h->opsBytes;
+  return BG_OK;
+}
+
+// bg_batch_export_compact without a host wait (the record of EVERY execute gathered inside a
+// pipelined step): the size, scan and write kernels go on the handle's export stream behind the
+// last execute's traceback; the slot's next execute waits for them (readDone), and `after` (a
+// stream of the handle's device, may be null) waits for them too, so a collective queued there
+// reads a finished record.
+extern "C" int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t cap, void* after) {
+  if (!h || !dst) return BG_E_ARG;
+  if (!h->prepared || !h->executed) return BG_E_NO_BATCH;
+  const uint64_t n = h->npairs;
+  if (cap < 32 + n * sizeof(bg_compact_hdr) + h->opsBytes) return BG_E_ARG;
+  BG_HIP(hipSetDevice(h->device));
+  Slot& S = h->slot[h->lastSlot];
+  if (!h->dlS) h->dlS = group_stream(h, kSDl);
+  if (!h->dlS) return BG_E_HIP;
+  hipStream_t xs = h->dlS;
+  if (!h->compactSizes.ensure(8 * (n + 1))) return BG_E_NOMEM;
+  BgCompactArgs E;
+  E.pairs = h->pairs.as<BgPair>();
+  E.results = S.results.as<BgResult>();
+  E.recs = h->recs.as<BgPairResultDev>();
+  E.ops = S.ops.as<uint8_t>();
+  E.sizes = h->compactSizes.as<uint64_t>();
+  E.dst = static_cast<uint8_t*>(dst);
+  E.npairs_caller = n;
+  E.nplan = (int32_t)h->plan.size();
+  E.mode = h->mode;
+  void* args[] = {&E};
+  if (S.inflight) BG_HIP(hipStreamWaitEvent(xs, S.finDone, 0));
+  BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), xs));
+  const unsigned gs = (unsigned)(((uint64_t)E.nplan + 255) / 256);
+  if (gs) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(gs), dim3(256), args, 0, xs));
+  BG_HIP(hipLaunchKernel(bg_compact_scan_kernel_ptr(), dim3(1), dim3(1024), args, 0, xs));
+  const unsigned gw = (unsigned)E.nplan + (unsigned)((n + 255) / 256) + 1;
+  BG_HIP(hipLaunchKernel(bg_compact_write_kernel_ptr(), dim3(gw), dim3(256), args, 0, xs));
+  BG_HIP(hipEventRecord(S.readDone, xs));
+  S.readPending = true;
+  h->compactExec = -1;             // the sizes now belong to this record
+  if (after) BG_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(after), S.readDone, 0));
   return BG_OK;
 }
 

@@ -360,12 +360,8 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
   for (size_t p = lo; p < hi && fail.load(std::memory_order_relaxed) == BG_OK; ++p) {
     const bg_compact_hdr& h = hd[p];
     const uint64_t ncore = (uint64_t)h.len - h.npre - h.ntail;
-    // BG_COMPACT_DEBUG: name the record that fails a check (stderr)
     auto bad = [&](int why) {
-      if (std::getenv("BG_COMPACT_DEBUG"))
-        std::fprintf(stderr, "compact_expand: pair %zu check %d: status %u len %u npre %u ntail %u start %u %u end %u %u n %zu %zu\n",
-                     p, why, (unsigned)h.status, (unsigned)h.len, (unsigned)h.npre, (unsigned)h.ntail,
-                     (unsigned)h.start1, (unsigned)h.start2, (unsigned)h.end_i, (unsigned)h.end_j, n1[p], n2[p]);
+      (void)why;
       fail.store(BG_E_ARG, std::memory_order_relaxed);
     };
     if ((uint64_t)h.npre + h.ntail > h.len || h.len > n1[p] + n2[p] || h.ops_off + (ncore + 3) / 4 > opsBytes ||

@@ -167,7 +167,6 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
   const int n1 = P.n1, n2 = P.n2, nst = P.nstrips, NC = P.nc;
   // concurrent exit pass (bg_split.hip): it waits for this DP's data only once every workgroup of
   // the DP is resident, so its workers can never hold the CUs this DP still needs
-  if (A.prio) __builtin_amdgcn_s_setprio(1);
   const bool ckgOn = WIDE && CKPT && A.split != nullptr;
   if (ckgOn && threadIdx.x == 0) __hip_atomic_fetch_add(A.resident, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (nst == 0) return;
@@ -404,7 +403,6 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
         if constexpr (IN == 0) {
           const int j = 32 * g + l32;
           inV = wadd(row0_M(mode, j, a, b), -wmul(a, j));                    // M'(0, j)
-          for (int z = 0; z < A.wide_pace; ++z) __builtin_amdgcn_s_sleep(1);
         } else if constexpr (IN == 1) {
           const int sq = hb + g;
           if (g < nh && pc < sq + 1) {

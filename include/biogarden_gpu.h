@@ -31,7 +31,9 @@
 extern "C" {
 #endif
 
-#define BG_ABI_VERSION 1
+/* 2: bg_stats gained `grouped` / `group_pairs` (a caller built against version 1 has a smaller
+ * struct: use bg_get_stats_sized, which writes only the bytes the caller's struct holds). */
+#define BG_ABI_VERSION 2
 
 typedef enum bg_mode {
   BG_GLOBAL = 0,
@@ -177,7 +179,11 @@ typedef struct bg_stats {
   int32_t group_pairs;     /* pairs per wave of the grouped DP (4 or 2), 0: not grouped */
 } bg_stats;
 
+/* Writes the whole bg_stats of this header (ABI version 2). */
 int bg_get_stats(bg_aligner* h, bg_stats* out);
+/* Writes min(size, sizeof(bg_stats)) bytes of it: a caller built against an older, smaller
+ * bg_stats passes its own sizeof and gets the fields it knows, nothing past its struct. */
+int bg_get_stats_sized(bg_aligner* h, bg_stats* out, size_t size);
 
 /* Split traceback of the last execute (few long pairs, linear gaps): pairs whose
  * walk was cut at strip boundaries, strips whose walks the stitching took, traceback moves the
@@ -229,6 +235,18 @@ int bg_profile_end(bg_aligner* h, float* avg_dp_ms, float* avg_finish_ms, int* e
  * of them.  bg_compact_expand rebuilds bg_batch_fetch's output from it and the input sequences.
  * dst = NULL: computes the record on the device (waits for the execute) and returns its exact
  * size in *bytes; then call again with dst (device memory of the handle's GPU, *bytes >= size). */
+/* The record's largest size for the prepared batch (32 + npairs x sizeof(bg_compact_hdr) + every
+ * pair's ops at ceil((n1 + n2) / 4)): the capacity bg_batch_export_compact_async needs. */
+int bg_batch_export_compact_bound(bg_aligner* h, size_t* bytes);
+/* bg_batch_export_compact of the last execute WITHOUT a host wait, for callers that gather every
+ * execute's record inside a pipelined step (the strong-scaling form of SURVEY §8(d)): the record
+ * is written to dst (device memory of the handle's GPU, cap >= the bound above) on the handle's
+ * export stream after that execute's traceback.  The handle's next execute into the same arena
+ * slot waits for it.  after (a hipStream_t of the same device, or NULL) is made to wait for the
+ * record, so a collective queued on it afterwards sends a finished record.  The record's own size
+ * is 32 + npairs x sizeof(bg_compact_hdr) + its header's ops bytes (u64 [2]); the bytes past it
+ * are unspecified. */
+int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t cap, void* after);
 typedef struct bg_compact_hdr {
   int32_t status, score;
   uint64_t ops_off;  /* into the ops area */
@@ -311,6 +329,43 @@ int bg_set_tuning(bg_aligner* h, int R, int waves);
  * kernel of execute k overlaps the DP kernel of execute k+1 (two HIP streams); 1 serialises.
  * Takes effect at the next bg_batch_prepare. */
 int bg_set_pipeline(bg_aligner* h, int depth);
+
+/* Per-handle options of the planner and the traceback (take effect at the next bg_batch_prepare /
+ * bg_batch_execute).  -1 restores the automatic choice.  The environment variable BG_OPTIONS
+ * ("name=value,...", names as below without the BG_OPT_ prefix, lower case) is read once per
+ * handle at bg_aligner_new, for tools that cannot call this. */
+enum {
+  BG_OPT_GROUPED = 0,            /* grouped DP (short reads sharing a reference): 0 never, 1 at any
+                                    fill, -1 when the groups fill (default) */
+  BG_OPT_GROUP_PAIRS = 1,        /* pairs per wave of the grouped DP: 2 or 4 (-1: 4 when the reads
+                                    fit 16 lanes x 10 rows) */
+  BG_OPT_GROUP_WAVES = 2,        /* waves per workgroup of the grouped DP, 1..16 (-1: 4) */
+  BG_OPT_WIDE_WAVES = 3,         /* waves per workgroup of a WIDE pair, 1..4 (-1: 4) */
+  BG_OPT_FIN_WAVES = 4,          /* traceback workgroup waves (walker + helpers), 1..4 */
+  BG_OPT_FIN_SLOTS = 5,          /* recomputed-chunk slots of a traceback workgroup, 0 = all */
+  BG_OPT_FIN_SYNC = 6,           /* 1: recomputation at a workgroup barrier (no helper waves) */
+  BG_OPT_FIN_SELFSERVE = 7,      /* 1: the walker recomputes every chunk it misses itself */
+  BG_OPT_SPLIT = 8,              /* split traceback of few long pairs: 0 never (-1: automatic) */
+  BG_OPT_SPLIT_SEGMENT = 9,      /* chunks per segment of the split traceback's exit pass */
+  BG_OPT_SPLIT_CONCURRENT = 10,  /* the exit pass beside the DP: 0 never, 1 always (-1: when no
+                                    other execute's DP is in flight) */
+  BG_OPT_SPLIT_WAIT_MS = 11,     /* the concurrent exit pass's wait bound per input (-1: 500) */
+  BG_OPT_TWO_DP_STREAMS = 12,    /* WIDE batches: consecutive DPs on two streams: 0 never */
+  BG_OPT_WAIT_MS = 13,           /* bound of every spin of a traceback on another wave (-1: 2000
+                                    ms); past it the pair ends with BG_INTERNAL and
+                                    bg_wait_diag records where */
+  BG_OPT_COUNT = 14
+};
+int bg_set_option(bg_aligner* h, int key, int value);
+int bg_get_option(bg_aligner* h, int key, int* value);
+/* The last execute's traceback wait that ran out (status BG_INTERNAL), up to n of its 18 words;
+ * all zero when none did.  [0] kind: 1 the walker waited for a recomputed chunk, 2 the walker
+ * waited for the slot lock, 3 a helper waited for it, 4 the walker recomputed one chunk over and
+ * over; [1] pair (plan order), [2] wave, [3] awaited chunk (strip << 16 | chunk), [4] its map
+ * entry, [5] slots being filled (bit per slot), [6] lock word, [7] / [8] the walker's row and
+ * column, [9] its recomputations of the chunk, [10..17] the slots' chunks.  Waits for the handle's
+ * work.  Not a reference interface: the evidence for a defect. */
+int bg_wait_diag(bg_aligner* h, uint32_t* out, size_t n);
 
 /* Kernel selection for tests and benchmarks (default 7).  Bit 0: allow the tagged linear kernel
  * (else the mask-trace kernel); bit 1: with it, run the score-only DP and recompute the chunks

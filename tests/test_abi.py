@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
 def test_host_only_entry_points():
     from biogarden_amd import _native
     L = _native.lib()
-    assert L.bg_abi_version() == 1
+    assert L.bg_abi_version() == 2
     assert L.bg_status_string(0) == b"ok"
     assert L.bg_status_string(1) == b"InvalidArgumentRange"
     sc = _native.BgScoring()

@@ -268,16 +268,14 @@ def test_traceback_walker_self_service(aligner, oracle, slots):
              (base, base[:1500] + base[4000:]), (base, mutate(rng, base, DNA, 0.15)),
              (base, base), (base, mutate(rng, base, DNA, 0.01))]
     expect = [oracle.align("semiglobal", s1, s2, "blosum62", -1, -2, exact=True) for s1, s2 in pairs]
-    os.environ["BG_FIN_SELFSERVE"] = "1"
-    os.environ["BG_FIN_SLOTS"] = slots
     try:
-        for R, W in ((8, 16), (2, 4)):
-            aligner.set_tuning(R, W)
-            res = aligner.align_batch("semiglobal", pairs, score.blosum62, -1, -2)
-            for e, r in zip(expect, res):
-                assert r.status in (0, 4), (R, W, r.status)
-                assert (e[1], e[2], e[3]) == (r[0], bytes(r[1].chain), bytes(r[2].chain)), (R, W)
+        with aligner.options(fin_selfserve=1, fin_slots=int(slots)):
+            for R, W in ((8, 16), (2, 4)):
+                aligner.set_tuning(R, W)
+                res = aligner.align_batch("semiglobal", pairs, score.blosum62, -1, -2)
+                assert aligner._h.wait_diag() is None, (R, W, aligner._h.wait_diag())
+                for e, r in zip(expect, res):
+                    assert r.status in (0, 4), (R, W, r.status)
+                    assert (e[1], e[2], e[3]) == (r[0], bytes(r[1].chain), bytes(r[2].chain)), (R, W)
     finally:
-        os.environ.pop("BG_FIN_SELFSERVE", None)
-        os.environ.pop("BG_FIN_SLOTS", None)
         aligner.set_tuning(0, 0)

@@ -215,3 +215,39 @@ def test_compact_gather_over_rccl_world1():
     finally:
         h.close()
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("local", -11, -1)])
+def test_compact_export_async_pipelined(mode, a, b):
+    """bg_batch_export_compact_async (the strong bench step): every execute's record exported
+    without a host wait into a buffer of its own, six executes pipelined over three arena slots
+    (each slot's next execute waits for its export), torch's stream ordered after each record;
+    every record equals the synchronous export of the same batch, bytes for bytes, and fits the
+    bound."""
+    import struct
+
+    import torch
+    from biogarden_amd import _native
+    pairs = _pairs(41 + len(mode))
+    h = _native.Handle(0)
+    try:
+        h.set_pipeline(3)
+        h.prepare(mode, pairs, _native.builtin_scoring(_native.BG_BLOSUM62), a, b)
+        cap = h.export_compact_bound()
+        bufs = [torch.full((cap,), 0xAB, dtype=torch.uint8, device="cuda") for _ in range(6)]
+        stream = torch.cuda.current_stream()
+        for buf in bufs:
+            h.execute()
+            h.export_compact_async(buf.data_ptr(), cap, stream.cuda_stream)
+        copies = [buf.cpu() for buf in bufs]          # on torch's stream: after each record
+        ref = _compact(h)
+        fetched = h.fetch()
+    finally:
+        h.close()
+    assert len(ref) <= cap
+    for c in copies:
+        raw = c.numpy().tobytes()
+        _, n, ops, _ = struct.unpack_from("<4Q", raw, 0)
+        assert 32 + 48 * n + ops == len(ref)
+        assert raw[:len(ref)] == ref
+    assert _native.expand_compact(ref, pairs) == fetched

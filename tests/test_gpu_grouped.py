@@ -2,7 +2,7 @@
 (P = 4: one per 16-lane DPP row; P = 2: 32 lanes each), and the traceback recomputes a pair's
 chunks as 64 / P-lane jobs (bg_finish.h recompute_grp).  Results must not change: score and both
 strings against the oracle, and identical to the one-wave-per-pair path (BG_GROUPED=0) over
-whole batches, at both P and every R the planner picks ((64 / P) R >= the longest read), in the
+whole batches (bg_set_option grouped = 0), at both P and every R the planner picks ((64 / P) R >= the longest read), in the
 four linear-path modes, with references shorter than a chunk, one column long, and groups with
 empty rows."""
 import os
@@ -18,31 +18,21 @@ pytestmark = pytest.mark.gpu
 def _align(mode, pairs, a, b, grouped, P=""):
     from biogarden_amd.alignment import score
     from biogarden_amd.alignment.aligner import SequenceAligner
-    env = {"BG_GROUPED": grouped, "BG_GRP_P": P}
-    old = {k: os.environ.get(k) for k in env}
-    for k, v in env.items():
-        if v:
-            os.environ[k] = v
-        else:
-            os.environ.pop(k, None)
     al = SequenceAligner(0)
     try:
+        al.set_option("grouped", int(grouped) if grouped else None)
+        al.set_option("group_pairs", int(P) if P else None)
         res = al.align_batch(mode, pairs, score.blosum62, a, b)
         return res, al.stats()
     finally:
         al.close()
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
 
 
 def _key(r):
     return (r.status, r[0], bytes(r[1].chain), bytes(r[2].chain))
 
 
-@pytest.mark.parametrize("P", ["8", "4", "2"])
+@pytest.mark.parametrize("P", ["4", "2"])
 def test_grouped_C4_slice_matches_ungrouped(oracle, P):
     from tools import workloads as w
     pairs = w.c4_pairs(nrefs=8, reads_per_ref=131)          # 131 per reference: partial groups
@@ -62,7 +52,7 @@ def test_grouped_C4_slice_matches_ungrouped(oracle, P):
 
 def _edge_pairs(seed, R, mode, P):
     rng = random.Random(seed)
-    top = (16 if P == 8 else 64 // P) * R
+    top = (64 // P) * R
     reflens = [1, 5, 63, 64, 65, 127, 200, 700]
     if mode == "fitting":                                   # seq2 fits in seq1 (n2 <= n1)
         reflens = [1, 2, 5, max(1, top // 4), max(1, top // 2), top - 1, top]
@@ -85,7 +75,7 @@ def _edge_pairs(seed, R, mode, P):
     return pairs
 
 
-@pytest.mark.parametrize("P", [8, 4, 2])
+@pytest.mark.parametrize("P", [4, 2])
 @pytest.mark.parametrize("R", [2, 3, 5, 8, 10])
 @pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("global", -2, -2), ("fitting", -1, -1),
                                       ("overlap", -1, -3)])
@@ -97,6 +87,31 @@ def test_grouped_edges_vs_oracle(oracle, R, mode, a, b, P):
     ref, _ = _align(mode, pairs, a, b, "0")
     diff = [p for p in range(len(pairs)) if _key(res[p]) != _key(ref[p])]
     assert not diff, diff[:10]
+
+
+@pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("global", -2, -2)])
+def test_grouped_batch_with_empty_pairs(oracle, mode, a, b):
+    """Empty reads and empty references inside a grouped batch: the planner leaves them out of
+    every group (their results are decided without a DP) while the grouped layout re-bases the
+    trace arena; their results, and every grouped pair's, equal the ungrouped run and the oracle."""
+    rng = random.Random(0xE0 + len(mode))
+    ref = rand_seq(rng, 700, DNA)
+    pairs = []
+    for k in range(80):
+        o = rng.randint(0, 550)
+        pairs.append((mutate(rng, ref[o:o + 150], DNA, 0.05), ref))
+        if k % 13 == 0:
+            pairs.append((b"", ref))
+        if k % 17 == 0:
+            pairs.append((rand_seq(rng, 120, DNA), b""))
+    pairs.append((b"", b""))
+    res, st = _align(mode, pairs, a, b, "1")
+    assert st["grouped"] > 0, st
+    ref_res, st0 = _align(mode, pairs, a, b, "0")
+    assert st0["grouped"] == 0, st0
+    diff = [p for p in range(len(pairs)) if _key(res[p]) != _key(ref_res[p])]
+    assert not diff, diff[:10]
+    check_results(oracle, mode, pairs, res, "blosum62", a, b)
 
 
 def test_grouping_declines_distinct_references(aligner, oracle):

@@ -400,7 +400,7 @@ def _long_gap_pairs(rng):
 
 @pytest.mark.parametrize("mode,a,b", [("semiglobal", -1, -2), ("global", -2, -2), ("overlap", -1, -1)])
 def test_traceback_async_matches_barriers_and_oracle(aligner, oracle, mode, a, b):
-    """The helper-wave recomputation (default) and the barrier form (BG_FIN_SYNC=1) give the
+    """The helper-wave recomputation (default) and the barrier form (bg_set_option fin_sync = 1) give the
     oracle's strings on long-gap paths, at the metric geometry and at a short-strip one."""
     from biogarden_amd.alignment import score
     rng = random.Random(0xA5C)
@@ -410,14 +410,11 @@ def test_traceback_async_matches_barriers_and_oracle(aligner, oracle, mode, a, b
         for R, W in ((8, 16), (2, 4)):
             aligner.set_tuning(R, W)
             for sync in (False, True):
-                if sync:
-                    os.environ["BG_FIN_SYNC"] = "1"
-                else:
-                    os.environ.pop("BG_FIN_SYNC", None)
+                aligner.set_option("fin_sync", 1 if sync else None)
                 res = aligner.align_batch(mode, pairs, score.blosum62, a, b)
                 for e, r in zip(expect, res):
                     assert r.status in (0, 4), (R, W, sync, r.status)
                     assert (e[1], e[2], e[3]) == (r[0], bytes(r[1].chain), bytes(r[2].chain)), (R, W, sync)
     finally:
-        os.environ.pop("BG_FIN_SYNC", None)
+        aligner.set_option("fin_sync", None)
         aligner.set_tuning(0, 0)

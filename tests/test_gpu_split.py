@@ -26,13 +26,12 @@ def _pairs(rng, shapes, rate=0.15):
     return out
 
 
-def _run(pairs, mode, a, b, R=0, scoring=None, env=None, monkeypatch=None, executes=1, diag=None):
+def _run(pairs, mode, a, b, R=0, scoring=None, opts=None, executes=1, diag=None):
     from biogarden_amd import _native
-    if env and monkeypatch is not None:
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
     h = _native.Handle(0)
     try:
+        for k, v in (opts or {}).items():
+            h.set_option(k, v)
         if R:
             h.set_tuning(R, 0)
         sc = scoring or _native.builtin_scoring(_native.BG_BLOSUM62)
@@ -78,7 +77,7 @@ def test_split_segment_lengths(oracle, monkeypatch, segc):
     segment boundary of a strip (1), at odd positions (3), or never arise (one segment)."""
     rng = random.Random(int(segc))
     pairs = _pairs(rng, [(9000, 9100), (6000, 2500)], rate=0.25)
-    got, st, sp = _run(pairs, "semiglobal", -1, -2, env={"BG_SPLIT_SEGC": segc}, monkeypatch=monkeypatch)
+    got, st, sp = _run(pairs, "semiglobal", -1, -2, opts={"split_segment": int(segc)})
     _check(oracle, "semiglobal", pairs, got, -1, -2)
     assert st["split"] == 1 and sp["tail_moves"] == 0 and sp["strips_taken"] > 0, sp
 
@@ -88,8 +87,7 @@ def test_split_matches_whole_walk(monkeypatch):
     rng = random.Random(7)
     pairs = _pairs(rng, [(11000, 10000), (8000, 300), (5000, 9000)], rate=0.3)
     split, st1, _ = _run(pairs, "semiglobal", -1, -2, executes=3)
-    monkeypatch.setenv("BG_SPLIT", "0")
-    whole, st0, _ = _run(pairs, "semiglobal", -1, -2)
+    whole, st0, _ = _run(pairs, "semiglobal", -1, -2, opts={"split": 0})
     assert st1["split"] == 1 and st0["split"] == 0
     assert split == whole
 
@@ -128,16 +126,14 @@ def test_split_exit_pass_beside_dp(oracle, monkeypatch):
     the concurrent pass did the items (so the granule hand-off, not the fallback, is tested)."""
     rng = random.Random(23)
     pairs = _pairs(rng, [(20000, 19000), (9000, 9500)], rate=0.2)
-    monkeypatch.setenv("BG_SPLIT_CONC", "1")
     dg = {}
-    conc, st, sp = _run(pairs, "semiglobal", -1, -2, executes=3, diag=dg)
+    conc, st, sp = _run(pairs, "semiglobal", -1, -2, executes=3, diag=dg, opts={"split_concurrent": 1})
     print("conc diag", dg, "split", sp, flush=True)
     _check(oracle, "semiglobal", pairs, conc, -1, -2)
     assert st["split"] == 1 and sp["tail_moves"] == 0 and sp["pairs_overflow"] == 0, sp
     assert dg["abandoned"] == 0 and dg["not_resident"] == 0, dg
     assert sp["items_beside_dp"] > 0, sp
-    monkeypatch.setenv("BG_SPLIT_CONC", "0")
-    post, _, sp0 = _run(pairs, "semiglobal", -1, -2)
+    post, _, sp0 = _run(pairs, "semiglobal", -1, -2, opts={"split_concurrent": 0})
     assert sp0["items_beside_dp"] == 0 and sp0["tail_moves"] == 0, sp0
     assert post == conc
 
@@ -149,12 +145,12 @@ def test_split_pipelined_two_dp_streams(oracle, monkeypatch, depth, conc):
     other DP is in flight), forced on, or off; every pipeline depth returns the reference's answer
     for the last execute."""
     from biogarden_amd import _native
-    if conc is not None:
-        monkeypatch.setenv("BG_SPLIT_CONC", conc)
     rng = random.Random(100 + depth)
     pairs = _pairs(rng, [(15000, 14000), (6000, 300)], rate=0.2)
     h = _native.Handle(0)
     try:
+        if conc is not None:
+            h.set_option("split_concurrent", int(conc))
         h.set_pipeline(depth)
         h.prepare("semiglobal", pairs, _native.builtin_scoring(_native.BG_BLOSUM62), -1, -2)
         for _ in range(5):
