@@ -35,7 +35,7 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
 # bg_set_option keys (include/biogarden_gpu.h BG_OPT_*), by their BG_OPTIONS names
 OPTIONS = ("grouped", "group_pairs", "group_waves", "wide_waves", "fin_waves", "fin_slots",
            "fin_sync", "fin_selfserve", "split", "split_segment", "split_concurrent",
-           "split_wait_ms", "two_dp_streams", "wait_ms")
+           "split_wait_ms", "two_dp_streams", "wait_ms", "span")
 
 
 class NativeUnavailable(RuntimeError):
@@ -428,7 +428,7 @@ class Handle:
     def export_compact_async(self, device_ptr, cap, after_stream=None):
         """bg_batch_export_compact_async: the last execute's compact record into device memory
         without a host wait; after_stream (a raw hipStream_t, e.g. torch's current stream's
-        cuda_stream) waits for it."""
+        cuda_stream; 0 / None = the null stream) waits for it."""
         check(lib().bg_batch_export_compact_async(self._p, ctypes.c_void_p(device_ptr), cap,
                                                   ctypes.c_void_p(after_stream or 0)))
 

@@ -274,10 +274,24 @@ __device__ __forceinline__ int ck_map_idx(int s, int c) { return ((s & 15) << 4)
 __device__ __forceinline__ bool wait_expired(const BgFinishArgs& F, unsigned long long t0) {
   return (long long)(__builtin_amdgcn_s_memrealtime() - t0) > (long long)F.waitTicks;
 }
+// The slot lock of the asynchronous traceback (sh[36]): lane 0 tries, the wave decides uniformly
+// (SGPR loop state, so no register of the loops around it is taken); false when the wait bound
+// ran out.  Holders keep it for a slot scan of straight-line code only.
+__device__ __forceinline__ bool slot_lock(const BgFinishArgs& F, int* lk, int lane) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  for (int sp = 0;; ++sp) {
+    int got = 0;
+    if (lane == 0) got = __hip_atomic_exchange(lk, 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0;
+    if (__builtin_amdgcn_readfirstlane(got)) return true;
+    __builtin_amdgcn_s_sleep(1);
+    if ((sp & 255) == 255 && wait_expired(F, t0)) return false;
+  }
+}
+
 // The first wait of an execute that ran out writes where it stood (one lane; include/
 // biogarden_gpu.h bg_wait_diag): the kind, the pair, the wave, the awaited key, its map entry,
 // the slots' filling flags and keys, the lock word, the walker's cell and its recomputations
-__device__ __noinline__ void wait_diag(const BgFinishArgs& F, int kind, int pidx, int wave, int key,
+__device__ __forceinline__ void wait_diag(const BgFinishArgs& F, int kind, int pidx, int wave, int key,
                                        const unsigned* ckMap, int* sh, int nSlots, int k, int l,
                                        int selfN) {
   if (!F.wdiag) return;
@@ -901,10 +915,12 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   if (async) {
     if (tid == 0) {
       sh[32] = preDone ? 1 : 0; sh[33] = -1; sh[34] = k; sh[35] = l; sh[36] = 0; sh[37] = 0; sh[56] = -1;
+      sh[59] = 0;                        // a wait that ran out: kind, key, recomputations, row, column
       for (int z = 0; z < 8; ++z) { sh[40 + z] = -1; sh[48 + z] = 0; }
     }
     __syncthreads();
   }
+  int helperLost = 0;
   if (async && wid != 0) {
     const int NCp = P.nc, NSp = P.nstrips;
     auto enc = [](int key, int z) { return (unsigned)((key >> 16) << 20) | (unsigned)((key & 0xffff) << 4) | (unsigned)z; };
@@ -915,23 +931,10 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     int idle = 0;
     for (;;) {
       if (__hip_atomic_load(&sh[32], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-      int key = -1, zz = -1, lockLost = 0;
-      if (lane == 0) {
-        // the lock is held for a slot scan only; past the wait bound this helper stops helping
-        // (the walker serves itself) and the diag names the holder's state
-        const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
-        for (int sp = 1; __hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0; ++sp) {
-          help_pause(1);
-          if ((sp & 255) == 0 && wait_expired(F, tl0)) { lockLost = 1; break; }
-        }
-      }
-      if (uni(__shfl(lockLost, 0, 64))) {
-        if (lane == 0)
-          wait_diag(F, BG_WD_LOCK_HELPER, P.index, wid, -1, ckMap, sh, nSlots,
-                    __hip_atomic_load(&sh[34], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
-                    __hip_atomic_load(&sh[35], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP), 0);
-        break;
-      }
+      int key = -1, zz = -1;
+      // past the wait bound this helper stops helping (the walker serves itself) and the diag
+      // names the lock's state
+      if (!slot_lock(F, &sh[36], lane)) { helperLost = 1; break; }
       if (lane == 0) {
         const int req = __hip_atomic_load(&sh[33], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const int kw = __hip_atomic_load(&sh[34], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1035,6 +1038,11 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
         __hip_atomic_store(&sh[48 + zz], 0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
+  }
+  if (helperLost && lane == 0 &&
+      __hip_atomic_compare_exchange_strong(&sh[59], &helperLost, BG_WD_LOCK_HELPER, __ATOMIC_RELAXED,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+    sh[60] = -1; sh[61] = 0; sh[62] = sh[34]; sh[63] = sh[35];
   }
   for (;;) {
     int reqS = -1, reqB0 = 0, done = preDone ? 1 : 0;
@@ -1219,15 +1227,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
                 break;
               }
               if (it >= selfPolls && (it - selfPolls) % 64 == 0) {
-                int zz = -1, lockLost = 0;
-                if (lane == 0) {
-                  const unsigned long long tl0 = __builtin_amdgcn_s_memrealtime();
-                  for (int sp = 1; __hip_atomic_exchange(&sh[36], 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0; ++sp) {
-                    __builtin_amdgcn_s_sleep(1);
-                    if ((sp & 255) == 0 && wait_expired(F, tl0)) { lockLost = 1; break; }
-                  }
-                }
-                if (uni(__shfl(lockLost, 0, 64))) { why = BG_WD_LOCK_WALKER; break; }
+                int zz = -1;
+                if (!slot_lock(F, &sh[36], lane)) { why = BG_WD_LOCK_WALKER; break; }
                 if (lane == 0) {
                   // in flight (flags first), then published meanwhile (the map second): see the
                   // helpers' candidate check
@@ -1307,7 +1308,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
             }
             if (!got) {
               // 5: BG_INTERNAL (no schedule reaches it), with the wait's record in bg_wait_diag
-              if (lane == 0) wait_diag(F, why, P.index, 0, key, ckMap, sh, nSlots, k, l, selfN);
+              // the record goes out after the walk (bg_wait_diag), where few registers are live
+              if (lane == 0) { sh[59] = why; sh[60] = key; sh[61] = selfN; sh[62] = k; sh[63] = l; }
               status = 5;
               done = 1;
               break;
@@ -1449,6 +1451,8 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     __syncthreads();
     tMiss += __builtin_readcyclecounter() - tm0;
   }
+  if (async && tid == 0 && sh[59])
+    wait_diag(F, sh[59], P.index, sh[59] == BG_WD_LOCK_HELPER ? -1 : 0, sh[60], ckMap, sh, nSlots, sh[62], sh[63], sh[61]);
   if (F.dbg && tid == 0) {
     u64* d = F.dbg + (size_t)P.index * 16;
     d[0] = __builtin_readcyclecounter() - tWalk0;

@@ -174,7 +174,7 @@ static const BgDebug& dbg_flags() {
 static const char* const kOptNames[BG_OPT_COUNT] = {
     "grouped", "group_pairs", "group_waves", "wide_waves", "fin_waves", "fin_slots", "fin_sync",
     "fin_selfserve", "split", "split_segment", "split_concurrent", "split_wait_ms",
-    "two_dp_streams", "wait_ms"};
+    "two_dp_streams", "wait_ms", "span"};
 
 // Host-side phases of prepare / fetch, accumulated per handle (bg_host_timing) and, with
 // BG_PREPARE_TIMING set, printed per call on stderr
@@ -212,6 +212,7 @@ struct Slot {
   // compact export): the next execute into this slot waits for it before its kernels write
   hipEvent_t readDone = nullptr;
   bool inflight = false, readPending = false;
+  bool dpPending = false;           // a DP queued by an execute that failed before its finDone
 };
 
 // The HIP streams of one handle, or of several handles on one device that share them
@@ -301,6 +302,7 @@ struct bg_aligner {
   int codesInLds = 0;
   int auxLdsOff = 0;
   int wide = 0;                    // tagged kernel: pairs spread over groups of workgroups
+  int span = 0;                    // ... of many-wave workgroups (fewer pairs than CUs, SPAN)
   // grouped DP (bg_grp_kernel.hip): short reads sharing a reference, `grouped` (P = 4 or 2) per
   // wave, 0 off; grpHost holds P plan indices per group (-1: an empty row)
   int grouped = 0, ngroups = 0;
@@ -428,6 +430,7 @@ static hipError_t drain(bg_aligner* h) {
   for (const Slot& S : h->slot) {
     if (S.inflight && (e = hipEventSynchronize(S.finDone)) != hipSuccess) return e;
     if (S.readPending && (e = hipEventSynchronize(S.readDone)) != hipSuccess) return e;
+    if (S.dpPending && (e = hipEventSynchronize(S.dpDone)) != hipSuccess) return e;
   }
   if (h->dlExec >= 0 && (e = hipEventSynchronize(h->dlDone)) != hipSuccess) return e;
   if (h->upPending && (e = hipEventSynchronize(h->upDone)) != hipSuccess) return e;
@@ -716,6 +719,9 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
       cells += (uint64_t)n1[p] * n2[p];
     }
   if (comp.empty() || comp.size() * 4 > (size_t)h->cus || h->tuneW) return false;
+  // more than a handful of pairs: throughput over the strip chain's latency (plan_span), unless
+  // the SPAN kernel is switched off
+  if (comp.size() * 16 > (size_t)h->cus && h->o(BG_OPT_SPAN, -1) != 0) return false;
   size_t maxn1 = 0;
   for (size_t p : comp) maxn1 = std::max(maxn1, n1[p]);
   if (maxn1 < 64 * 4 * 16) return false;                   // one workgroup's 16 waves suffice
@@ -819,6 +825,112 @@ static size_t fin_lds(const bg_aligner* h, int R, size_t np, int* win, int* area
 #define BG_FIN_R2 24.0
 #endif
 static constexpr double kFinR2 = BG_FIN_R2;
+
+// SPAN planner (linear checkpoint path, fewer pairs than CUs: one batch strong-scaled over
+// several GPUs, SURVEY §8(d) M at G = 2, 4, 8): each pair's strips are dealt over a group of
+// many-wave workgroups, W consecutive strips per workgroup and round, the boundary row handed to
+// the next workgroup through HBM (bg_dp_tag_kernel<R, 2, true>).  One pair per CU (the
+// one-workgroup plan) leaves cus - npairs CUs idle; the group spreads a pair over
+// cus * cells_p / cells CUs.  Per (R, W) the strip pipeline of every distinct pair shape is
+// simulated phase by phase as in plan_geometry (a strip starts two phases after the one above in
+// its workgroup, three across workgroups, and after its wave's previous strip ended; a phase with
+// a active waves per SIMD on the busiest workgroup of the group costs 64 * (2R + 2) * a *
+// (4 + 3 / a) cycles); the slowest pair's estimate decides, and the group plan is kept only when
+// it beats the same simulation at one workgroup per pair.  BG_OPT_SPAN: 0 never, 1 whenever the
+// batch qualifies.
+static double span_estimate(int S, int G, int W, int NC, int ops) {
+  const int GW = G * W;
+  std::vector<int> start(S), end(S), wg(S);
+  int P = 0;
+  for (int s = 0; s < S; ++s) {
+    wg[s] = (s % GW) / W;
+    int st = 0;
+    if (s) st = start[s - 1] + (wg[s] == wg[s - 1] ? 2 : 3);
+    if (s >= GW) st = std::max(st, end[s - GW]);
+    start[s] = st;
+    end[s] = st + NC;
+    P = std::max(P, end[s]);
+  }
+  std::vector<int> act((size_t)P * G, 0);
+  for (int s = 0; s < S; ++s)
+    for (int q = start[s]; q < end[s]; ++q) ++act[(size_t)q * G + wg[s]];
+  double T = 0.0;
+  for (int q = 0; q < P; ++q) {
+    int A = 0;
+    for (int g = 0; g < G; ++g) A = std::max(A, act[(size_t)q * G + g]);
+    const int a = std::max(1, (A + 3) / 4);
+    T += 64.0 * ops * a * (4.0 + 3.0 / a);
+  }
+  return T;
+}
+
+static bool plan_span(bg_aligner* h, const size_t* n1, const size_t* n2, size_t npairs, int* Rout,
+                      int* Wout) {
+  const int os = h->o(BG_OPT_SPAN, -1);
+  if (os == 0 || h->tuneW) return false;
+  std::vector<size_t> comp;
+  uint64_t cells = 0;
+  for (size_t p = 0; p < npairs; ++p)
+    if (h->prestatus[p] < 0 && n1[p] > 0 && n2[p] > 0) {
+      comp.push_back(p);
+      cells += (uint64_t)n1[p] * n2[p];
+    }
+  if (comp.empty() || comp.size() * 2 > (size_t)h->cus) return false;
+  size_t maxn1 = 0, maxn2 = 0;
+  for (size_t p : comp) { maxn1 = std::max(maxn1, n1[p]); maxn2 = std::max(maxn2, n2[p]); }
+  const int cand[] = {2, 3, 4, 5, 8, 10};
+  double best = 1e300, best1 = 1e300;
+  int bestR = 0, bestW = 0;
+  std::vector<int> groups(npairs, 0), bestGroups;
+  std::map<std::pair<std::pair<size_t, size_t>, int>, double> memo;
+  // relax: no candidate leaves a traceback wave's VGPRs beside the DP's on each SIMD
+  for (int relax = 0; relax < 2 && !bestR; ++relax)
+  for (int Rc : cand) {
+    if (h->tuneR && Rc != h->tuneR) continue;
+    const void* fn = bg_dp_kernel_tag_ptr(Rc, 2, 1);
+    if (!fn) continue;
+    const int vg = vgprs_of(fn);
+    const int fin = (h->depth > 1 && !relax) ? vgprs_of(fin_fn(h, Rc)) : 0;
+    const int ops = 2 * Rc + 2;
+    for (int Wc : {4, 8, 12, 16}) {
+      const int wps = (Wc + 3) / 4;
+      if (wps * vg + fin > 512) continue;
+      if (640 + (size_t)Wc * bg_dp_tag_wave_lds_bytes(Rc) > 160 * 1024) continue;
+      double T = 0.0, T1 = 0.0;
+      int total = 0;
+      memo.clear();
+      for (size_t p : comp) {
+        const int S = (int)((n1[p] + 64 * Rc - 1) / (64 * Rc));
+        const double share = (double)h->cus * ((double)n1[p] * n2[p]) / (double)cells;
+        const int G = std::max(1, std::min((int)share, (S + Wc - 1) / Wc));
+        groups[p] = G;
+        total += G;
+        const int NC = (int)(n2[p] / 64 + 2);
+        auto key = std::make_pair(std::make_pair(n1[p], n2[p]), G);
+        auto it = memo.find(key);
+        const double t = it != memo.end() ? it->second : (memo[key] = span_estimate(S, G, Wc, NC, ops));
+        T = std::max(T, t);
+        T1 = std::max(T1, span_estimate(S, 1, Wc, NC, ops));
+      }
+      if (total > h->cus) continue;
+      if (T < best * 0.99 || (T < best * 1.01 && Rc > bestR)) {
+        best = T; bestR = Rc; bestW = Wc; bestGroups = groups;
+      }
+      best1 = std::min(best1, T1);
+    }
+  }
+  if (!bestR) return false;
+  bool multi = false;
+  for (size_t p : comp) multi |= bestGroups[p] > 1;
+  if (!multi || (os < 0 && best > 0.9 * best1)) return false;
+  if (dbg_flags().plan)
+    std::fprintf(stderr, "plan span R %d W %d T %.4g (one workgroup per pair %.4g)\n", bestR, bestW, best, best1);
+  *Rout = bestR;
+  *Wout = bestW;
+  h->groupOf = bestGroups;
+  h->tagRow = 1;
+  return true;
+}
 
 static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncomp, int* Rout,
                           int* Wout) {
@@ -994,7 +1106,7 @@ static int prepare_impl(bg_aligner* h, int mode, size_t npairs, const uint8_t* c
   ++h->nPrepare;
   BG_HIP(drain(h));
   tm.mark(kPhSync, "sync");
-  for (Slot& S : h->slot) S.inflight = S.readPending = false;
+  for (Slot& S : h->slot) S.inflight = S.readPending = S.dpPending = false;
   h->dlExec = -1;
   h->execCount = 0;
   h->prepared = false;
@@ -1113,11 +1225,13 @@ plan_again:
   // of workgroups per pair in the tagged kernel's WIDE mode)
   int R = 8, W = 1;
   h->wide = 0;
+  h->span = 0;
   h->grouped = 0;
   std::vector<int> refOf;     // grouped DP: caller pair -> reference class (-1: not grouped)
   if (h->tag && h->ckpt && !h->finFlags) h->grouped = plan_grouped(h, npairs, n1, n2, s2, dmaxS2a, &R, &W, refOf);
   if (h->grouped) {
   } else if (h->tag && plan_wide(h, n1, n2, npairs, &R, &W)) h->wide = 1;
+  else if (h->tag && h->ckpt && !h->finFlags && plan_span(h, n1, n2, npairs, &R, &W)) h->span = 1;
   else plan_geometry(h, maxn1, maxn2, ncomp, &R, &W);
   if ((h->ckpt || h->ack) && ncomp &&
       ((maxn1 + 64 * R - 1) / (64 * R) >= BG_CK_MAX_STRIPS || maxn2 / 64 + 2 >= BG_CK_MAX_CHUNKS)) {
@@ -1233,11 +1347,11 @@ plan_again:
     oo += n1[p] + n2[p];
     P.ops_off = po;
     po += (n1[p] + n2[p] + 3) / 4;
-    P.wg_count = h->wide ? std::max(1, h->groupOf[p]) : 1;
-    P.prog_off = h->wide ? h->progWords : 0;
+    P.wg_count = (h->wide || h->span) ? std::max(1, h->groupOf[p]) : 1;
+    P.prog_off = (h->wide || h->span) ? h->progWords : 0;
     P.buf_rows = (int32_t)std::min<long>(h->bufAt[p].first, 0x7FFFFFFF);
     P.buf_cols = (int32_t)std::min<long>(h->bufAt[p].second, 0x7FFFFFFF);
-    if (h->wide) {
+    if (h->wide || h->span) {
       // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8
       // share one, MI355X_MICROARCH.md), so consecutive indices in the group (consecutive strips:
       // a boundary row handed through HBM) go to blocks of one XCD class, and the hand-offs stay
@@ -1381,7 +1495,7 @@ plan_again:
                     !h->splitBaseBuf.ensure(4 * (h->splitBases.size() + 1)))) ||
       (h->pglob && !h->profScratch.ensure((h->plan.size() + 1) * (size_t)h->W * h->kdim * 64 * 4 * 4)))
     return BG_E_NOMEM;
-  h->gridWgs = h->wide ? (int)h->wgmap.size() : h->grouped ? (h->ngroups + W - 1) / W : (int)h->plan.size();
+  h->gridWgs = (h->wide || h->span) ? (int)h->wgmap.size() : h->grouped ? (h->ngroups + W - 1) / W : (int)h->plan.size();
   for (int z = 0; z < h->depth; ++z) {
     Slot& S = h->slot[z];
     if (!S.trace.ensure(tro + 256) || !S.bndM.ensure(bo * 4 + 256) ||
@@ -1391,7 +1505,7 @@ plan_again:
         ((h->split || h->grouped) && !S.keys.ensure(16 * (h->plan.size() + 1))) ||
         (h->split && !S.xcnt.ensure(8 * ((size_t)h->plan.size() * h->splitXBlocks + 1))) ||
         (h->split && !S.split.ensure(h->splitInts * 4 + 256)) ||
-        (h->wide && !S.gprog.ensure(4 * ((size_t)h->progWords + 8))))
+        ((h->wide || h->span) && !S.gprog.ensure(4 * ((size_t)h->progWords + 8))))
       return BG_E_NOMEM;
     // WIDE checkpoint batches hand strip rows between workgroups as epoch-tagged granules: a
     // fresh arena is zeroed so that no stale tag (of another handle) can match an epoch
@@ -1499,7 +1613,7 @@ plan_again:
   }
   BG_HIP(hipMemcpyAsync(h->prof.p, prof.data(), prof.size() * 4, hipMemcpyHostToDevice, us));
   if (!h->plan.empty())
-    if (h->wide)
+    if (h->wide || h->span)
     BG_HIP(hipMemcpyAsync(h->wgmapBuf.p, h->wgmap.data(), sizeof(int2) * h->wgmap.size(),
                           hipMemcpyHostToDevice, us));
   BG_HIP(hipMemcpyAsync(h->pairs.p, h->plan.data(), sizeof(BgPair) * h->plan.size(),
@@ -1649,7 +1763,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   BG_HIP(hipEventRecord(e[0], ds));
   if (np) {
     void* fn = h->grouped ? bg_dp_grp_kernel_ptr(h->R, h->grouped)
-             : h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide, h->ckpt) : dp_fn(h, h->R);
+             : h->tag ? bg_dp_kernel_tag_ptr(h->R, h->wide ? 1 : h->span ? 2 : 0, h->ckpt) : dp_fn(h, h->R);
     if (!fn) return BG_E_ARG;
     BgDpArgs A;
     A.pairs = h->pairs.as<BgPair>();
@@ -1663,13 +1777,13 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.codes_in_lds = h->codesInLds;
     A.aux_lds_off = h->auxLdsOff;
     A.wgmap = h->wgmapBuf.as<int2>();
-    A.gprog = h->wide ? S.gprog.as<uint32_t>() : h->gprogBuf.as<uint32_t>();
+    A.gprog = (h->wide || h->span) ? S.gprog.as<uint32_t>() : h->gprogBuf.as<uint32_t>();
     A.dbg = nullptr;
     if (dbg_flags().dp && h->tag && h->dpDbg.ensure(64 * 4096)) {
       A.dbg = h->dpDbg.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, ds));
     }
-    if (h->wide) BG_HIP(hipMemsetAsync(S.gprog.p, 0, 4 * ((size_t)h->progWords + 8), ds));
+    if (h->wide || h->span) BG_HIP(hipMemsetAsync(S.gprog.p, 0, 4 * ((size_t)h->progWords + 8), ds));
     if (conc) {
       if (!S.resetDone) BG_HIP(hipEventCreateWithFlags(&S.resetDone, hipEventDisableTiming));
       BG_HIP(hipEventRecord(S.resetDone, ds));
@@ -1705,6 +1819,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   exMark("dp");
   BG_HIP(hipEventRecord(e[1], ds));
   BG_HIP(hipEventRecord(S.dpDone, ds));
+  S.dpPending = true;              // until the finish is queued behind it (finDone covers it)
   exMark("dp-events");
   // The traceback stream.  A WIDE batch (a few long pairs: C3) is traceback-bound and its walks
   // occupy a handful of CUs, so consecutive executes' tracebacks alternate between two streams
@@ -1900,6 +2015,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   BG_HIP(hipEventRecord(e[3], fs));
   BG_HIP(hipEventRecord(S.finDone, fs));
   S.inflight = true;
+  S.dpPending = false;
   exMark("fin-events");
   // asynchronous fetch: the results' download queued behind the traceback, on a stream (and
   // hardware queue) of its own, so it neither waits behind the next DPs nor delays the next
@@ -2122,7 +2238,7 @@ extern "C" int bg_get_stats(bg_aligner* h, bg_stats* o) {
   o->R = h->R;
   o->waves = h->W;
   o->affine = h->affine;
-  o->wide = h->wide;
+  o->wide = h->wide ? 1 : h->span ? 2 : 0;
   o->workgroups = h->gridWgs;
   o->tagged = h->tag;
   o->checkpoint = h->ckpt || h->ack;
@@ -2352,8 +2468,8 @@ extern "C" int bg_batch_export_compact_bound(bg_aligner* h, size_t* bytes) {
 // bg_batch_export_compact without a host wait (the record of EVERY execute gathered inside a
 // pipelined step): the size, scan and write kernels go on the handle's export stream behind the
 // last execute's traceback; the slot's next execute waits for them (readDone), and `after` (a
-// stream of the handle's device, may be null) waits for them too, so a collective queued there
-// reads a finished record.
+// stream of the handle's device; null = its null stream) waits for them too, so a collective
+// queued there reads a finished record.
 extern "C" int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t cap, void* after) {
   if (!h || !dst) return BG_E_ARG;
   if (!h->prepared || !h->executed) return BG_E_NO_BATCH;
@@ -2386,7 +2502,8 @@ extern "C" int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t ca
   BG_HIP(hipEventRecord(S.readDone, xs));
   S.readPending = true;
   h->compactExec = -1;             // the sizes now belong to this record
-  if (after) BG_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(after), S.readDone, 0));
+  // NULL is the device's null stream (torch's default current stream): a valid stream to order
+  BG_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(after), S.readDone, 0));
   return BG_OK;
 }
 

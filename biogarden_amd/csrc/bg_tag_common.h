@@ -203,7 +203,10 @@ __device__ __forceinline__ void tag_chunk(TagStrip<R>& S, const TagCtx& C, int c
 // TOP0 (strip 0, interior chunks): the row above is row 0, M'(0, j) = top0 + (j - t0) topStep
 // (aligner.rs:98-104 borders, linear in j for j >= 1), kept in a scalar register instead of one
 // broadcast LDS read per step — the read that makes single-strip batches (C4) LDS-bound.
-template <int R, int VAR, bool WIDE, bool TOP0 = false>
+// AGT: the boundary row goes out with agent-scope (sc1) stores, for a consumer in another
+// workgroup, possibly on another XCD (WIDE and SPAN); else plain stores (the same workgroup, or
+// the traceback after the kernel's end)
+template <int R, int VAR, bool WIDE, bool TOP0 = false, bool AGT = WIDE>
 __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int c) {
   const int a = C.a;
   const int t0 = c * BG_CHUNK;
@@ -281,7 +284,7 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
       const int v = C.ring[lane];
       const int nx = C.ring[64 + lane];
       if (C.mail) C.mail[lane] = v;
-      if constexpr (WIDE)
+      if constexpr (AGT)
         __hip_atomic_store(C.bndOut + (c - 1) * BG_CHUNK + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       else
         C.bndOut[(c - 1) * BG_CHUNK + lane] = v;

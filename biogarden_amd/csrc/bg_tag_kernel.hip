@@ -116,8 +116,15 @@ __host__ __device__ constexpr int tag_wave_ints() {
 // arena: ckpt[((s * NC + c) * (R + 1) + k) * 64 + lane] (k = R: topPrev).
 // WIDE: one workgroup of 4 waves per CU (one per SIMD), so a wave may hold up to 512 VGPRs: the
 // six conveyor-loop instantiations then run without spills (at 1024 threads they spilled 48 B/lane)
-template <int R, bool WIDE, bool CKPT>
-__global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A) {
+// WM (the pair's width): 0 one workgroup per pair; 1 WIDE, a group of lone-wave workgroups per pair
+// (few long pairs: the strip chain's latency); 2 SPAN, a group of many-wave workgroups per pair
+// (fewer pairs than CUs: throughput).  SPAN hands rows between workgroups as WIDE does (boundary
+// rows in HBM, agent-scope progress counters, at every W-th strip) and computes, polls and
+// stages codes as the one-workgroup path does (several waves per SIMD).
+template <int R, int WM, bool CKPT>
+__global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A) {
+  constexpr bool WIDE = WM != 0;          // a group of workgroups per pair
+  constexpr bool LONE = WM == 1;          // ... of one wave per SIMD
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int RW = ProfW<R>::v;
   const int lane = threadIdx.x & 63;
@@ -245,7 +252,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
     // (M'(i, j) >= M'(i, j - 1) in the frame) — and the lane holding row n1 hands it down as its
     // last row: the last strip runs the plain step instead of a select per row and step (1.8 % of
     // the metric DP's VALU).  Nothing reads those rows: the traceback never walks below row n1.
-    const bool repeatN1 = CKPT && !WIDE && lastStrip && C.orow != R - 1;
+    const bool repeatN1 = CKPT && !LONE && lastStrip && C.orow != R - 1;
     if (repeatN1) C.orow = R - 1;
     C.repeatN1 = repeatN1;
     const bool selRow = C.orow != R - 1;
@@ -313,7 +320,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
     //    only loads are issued a half ahead, so no wait of this loop waits on a fresh store.
     // The last strip reads whole blocks (two adjacent half slots, or 64 granules) and keeps the
     // ring path for its output row (row n1 may sit in any lane).
-    constexpr bool CONVMODE = WIDE && CKPT;
+    constexpr bool CONVMODE = LONE && CKPT;
     constexpr int KH = 2 * kMailSlots;                          // half slots per mailbox
     const int nh = 2 * nblk;                                     // halves handed down per strip
     const uint32_t ep = A.epoch;
@@ -517,7 +524,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
       int np0 = 0;
       if (0 < nblk)
         while ((int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < needBase + 1)
-          wide_poll_pause(np0);
+          poll_pause<LONE>(np0);
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       nbV = load_agent(bndAbove);
       pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -561,7 +568,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
           if (c + 1 < nblk) {
             int np1 = 0;
             while (pollV < needBase + c + 2) {
-              wide_poll_pause(np1);
+              poll_pause<LONE>(np1);
               pollV = (int)__hip_atomic_load(gProg + pwH, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
           }
@@ -576,11 +583,11 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
           if (WIDE && !mailIn) {
             int np2 = 0;
             while ((int)__hip_atomic_load(gProg + pw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need)
-              wide_poll_pause(np2);
+              poll_pause<LONE>(np2);
           } else {
             int np = 0;
             while (__hip_atomic_load(sProg + pw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
-              poll_pause<WIDE>(np);
+              poll_pause<LONE>(np);
           }
         }
         if (mailIn) {
@@ -599,7 +606,7 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
         const int needC = seq - kMailSlots;                      // consumer chunks finished
         int np = 0;
         while (__hip_atomic_load(sCons + w + 1, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < needC)
-          poll_pause<WIDE>(np);
+          poll_pause<LONE>(np);
         C.mail = mailbox + ((seq - 1) % kMailSlots) * 64;
       }
       if (dbgOn) tWait += __builtin_amdgcn_s_memtime() - tw0;
@@ -617,20 +624,20 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
                                ((unsigned long long)A.epoch << 32) | (uint32_t)(k < R ? S.Y[k] : S.topPrev),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (edge) score_chunk<R, TV_EDGE, WIDE>(S, C, c);
-        else if (lastStrip && selRow) score_chunk<R, TV_SEL, WIDE>(S, C, c);
+        if (edge) score_chunk<R, TV_EDGE, LONE, false, WIDE>(S, C, c);
+        else if (lastStrip && selRow) score_chunk<R, TV_SEL, LONE, false, WIDE>(S, C, c);
         else if (R <= 4 && s == 0) {
           // row 0 above: M'(0, j) for j >= 1 is linear (semiglobal / local / overlap: M = 0;
           // global / fitting: a + (j - 1) b)
           const bool flat = mode == BGK_SEMIGLOBAL || mode == BGK_LOCAL || mode == BGK_OVERLAP;
           C.topStep = flat ? -a : b - a;
           C.top0 = wadd(row0_M(mode, c * BG_CHUNK, a, b), -wmul(a, c * BG_CHUNK));
-          score_chunk<R, TV_FAST, WIDE, true>(S, C, c);
-        } else score_chunk<R, TV_FAST, WIDE>(S, C, c);
+          score_chunk<R, TV_FAST, LONE, true, WIDE>(S, C, c);
+        } else score_chunk<R, TV_FAST, LONE, false, WIDE>(S, C, c);
       } else {
-        if (edge) tag_chunk<R, TV_EDGE, WIDE>(S, C, c);
-        else if (lastStrip && selRow) tag_chunk<R, TV_SEL, WIDE>(S, C, c);
-        else tag_chunk<R, TV_FAST, WIDE>(S, C, c);
+        if (edge) tag_chunk<R, TV_EDGE, LONE>(S, C, c);
+        else if (lastStrip && selRow) tag_chunk<R, TV_SEL, LONE>(S, C, c);
+        else tag_chunk<R, TV_FAST, LONE>(S, C, c);
       }
       // publish.  LDS mailbox: the block's ds_writes precede the counter's in this wave's LDS
       // queue.  HBM: the chunk ends with the block store and R trace stores; at vmcnt(R) the
@@ -675,10 +682,11 @@ __global__ __launch_bounds__(WIDE ? 256 : 1024) void bg_dp_tag_kernel(BgDpArgs A
 }
 
 #define BG_TAG_INST(RR)                                                   \
-  template __global__ void bg_dp_tag_kernel<RR, false, false>(BgDpArgs);  \
-  template __global__ void bg_dp_tag_kernel<RR, true, false>(BgDpArgs);   \
-  template __global__ void bg_dp_tag_kernel<RR, false, true>(BgDpArgs);   \
-  template __global__ void bg_dp_tag_kernel<RR, true, true>(BgDpArgs);
+  template __global__ void bg_dp_tag_kernel<RR, 0, false>(BgDpArgs);      \
+  template __global__ void bg_dp_tag_kernel<RR, 1, false>(BgDpArgs);      \
+  template __global__ void bg_dp_tag_kernel<RR, 0, true>(BgDpArgs);       \
+  template __global__ void bg_dp_tag_kernel<RR, 1, true>(BgDpArgs);       \
+  template __global__ void bg_dp_tag_kernel<RR, 2, true>(BgDpArgs);
 BG_TAG_INST(2)
 BG_TAG_INST(3)
 BG_TAG_INST(4)
@@ -686,12 +694,15 @@ BG_TAG_INST(5)
 BG_TAG_INST(8)
 BG_TAG_INST(10)
 
+// wide: 0 one workgroup per pair, 1 WIDE (lone waves), 2 SPAN (checkpoint only)
 extern "C" void* bg_dp_kernel_tag_ptr(int R, int wide, int ckpt) {
   switch (R) {
 #define BG_TAG_CASE(RR)                                                                   \
     case RR:                                                                              \
-      if (ckpt) return wide ? (void*)&bg_dp_tag_kernel<RR, true, true> : (void*)&bg_dp_tag_kernel<RR, false, true>; \
-      return wide ? (void*)&bg_dp_tag_kernel<RR, true, false> : (void*)&bg_dp_tag_kernel<RR, false, false>;
+      if (ckpt) return wide == 2 ? (void*)&bg_dp_tag_kernel<RR, 2, true>                  \
+                     : wide ? (void*)&bg_dp_tag_kernel<RR, 1, true> : (void*)&bg_dp_tag_kernel<RR, 0, true>; \
+      if (wide == 2) return nullptr;                                                      \
+      return wide ? (void*)&bg_dp_tag_kernel<RR, 1, false> : (void*)&bg_dp_tag_kernel<RR, 0, false>;
     BG_TAG_CASE(2)
     BG_TAG_CASE(3)
     BG_TAG_CASE(4)

@@ -166,7 +166,8 @@ typedef struct bg_stats {
   int32_t dna;             /* 1: register profile (<= 4 symbols), 0: LDS profile */
   int32_t local;
   int32_t npairs;
-  int32_t wide;            /* 1: tagged kernel with each pair spread over a group of workgroups */
+  int32_t wide;            /* tagged kernel with each pair spread over a group of workgroups:
+                              1 of one wave per SIMD (WIDE), 2 of several (SPAN); 0 one per pair */
   int32_t workgroups;      /* DP grid size */
   int32_t checkpoint;      /* 1: score-only DP + traceback recomputing the chunks its path crosses */
   float dp_ms;             /* last execute: DP kernel time (HIP events on the handle's stream) */
@@ -242,8 +243,8 @@ int bg_batch_export_compact_bound(bg_aligner* h, size_t* bytes);
  * execute's record inside a pipelined step (the strong-scaling form of SURVEY §8(d)): the record
  * is written to dst (device memory of the handle's GPU, cap >= the bound above) on the handle's
  * export stream after that execute's traceback.  The handle's next execute into the same arena
- * slot waits for it.  after (a hipStream_t of the same device, or NULL) is made to wait for the
- * record, so a collective queued on it afterwards sends a finished record.  The record's own size
+ * slot waits for it.  after (a hipStream_t of the same device; NULL = that device's null stream)
+ * is made to wait for the record, so a collective queued on it afterwards sends a finished record.  The record's own size
  * is 32 + npairs x sizeof(bg_compact_hdr) + its header's ops bytes (u64 [2]); the bytes past it
  * are unspecified. */
 int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t cap, void* after);
@@ -354,7 +355,10 @@ enum {
   BG_OPT_WAIT_MS = 13,           /* bound of every spin of a traceback on another wave (-1: 2000
                                     ms); past it the pair ends with BG_INTERNAL and
                                     bg_wait_diag records where */
-  BG_OPT_COUNT = 14
+  BG_OPT_SPAN = 14,              /* fewer pairs than CUs: each pair over a group of many-wave
+                                    workgroups: 0 never, 1 whenever it applies (-1: when the
+                                    planner's estimate gains) */
+  BG_OPT_COUNT = 15
 };
 int bg_set_option(bg_aligner* h, int key, int value);
 int bg_get_option(bg_aligner* h, int key, int* value);
