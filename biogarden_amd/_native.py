@@ -582,7 +582,7 @@ class Group:
         batch needs (a streaming caller rotates a few; fresh buffers fault their pages in)."""
         # bg_group_collect always finishes the OLDEST batch and writes that batch's pair count of
         # results: any other ticket would size the buffers for the wrong batch
-        if not self._tickets or ticket is not self._tickets[0]:
+        if self._tickets and ticket is not self._tickets[0]:
             raise ValueError("collect() takes the oldest submitted ticket (submission order)")
         total, n = ticket[4], ticket[5]
         if bufs is not None and len(bufs[0]) >= n and len(bufs[1]) >= total and len(bufs[2]) >= total:
@@ -592,7 +592,8 @@ class Group:
             o1 = (ctypes.c_uint8 * max(total, 1))()
             o2 = (ctypes.c_uint8 * max(total, 1))()
         check(lib().bg_group_collect(self._p, res, o1, o2, max(total, 1) if bufs is None else len(o1)))
-        self._tickets.pop(0)
+        if self._tickets:
+            self._tickets.pop(0)
         return res, o1, o2
 
     def pending(self):

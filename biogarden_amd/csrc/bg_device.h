@@ -197,7 +197,7 @@ struct BgDpArgs {
   const int2* wgmap;       // tagged kernel, WIDE mode: per workgroup (plan index, index in group)
   uint32_t* gprog;         // tagged kernel, WIDE mode: global per-wave progress counters
   int32_t pstride;         // row stride of the int16 profile table (the batch's dense alphabet)
-  unsigned long long* dbg; // optional per-wave timestamps of the first strip (env BG_DP_TIMING):
+  unsigned long long* dbg; // optional per-wave timestamps of the first strip (env BG_DEBUG=dp):
                            // [gw * 8 + k], k: 0 strip, 1 start, 2 chunk 0 done, 3 end, 4 waited
   int32_t* prof_scratch;   // mask kernel, int32 profiles in HBM: kdim x 64 x R ints per (pair, wave)
   unsigned long long* gran;  // tagged WIDE checkpoint mode: strip-boundary rows as {value, epoch}
@@ -240,7 +240,7 @@ struct BgFinishArgs {
   const uint8_t* codes1;
   const uint8_t* codes2;
   const int32_t* profile;
-  unsigned long long* dbg;  // optional per-pair cycle counters (env BG_FINISH_TIMING)
+  unsigned long long* dbg;  // optional per-pair cycle counters (env BG_DEBUG=finish)
   // affine / local checkpoint traceback (bg_aff_kernel.hip): X boundary rows, alphabet size
   // (per-lane profile entries) and the ints of one wave's recompute area
   const int32_t* bndX;

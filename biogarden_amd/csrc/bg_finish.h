@@ -390,7 +390,7 @@ __device__ void recompute_chunk_aff(const BgFinishArgs& F, const BgPair& P, int 
 template <int R, bool AFFINE, int MODE, bool CK = false, int GRP = 0>
 __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const u64 tK0 = __builtin_readcyclecounter();       // BG_FINISH_TIMING: the kernel's phases
+  const u64 tK0 = __builtin_readcyclecounter();       // BG_DEBUG=finish: the kernel's phases
   const u64 tR0 = __builtin_amdgcn_s_memrealtime();
   constexpr int NW = AFFINE ? 4 : 2;
   constexpr int ROWS = BG_WAVE * R;
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     for (int x = threadIdx.x; x < kCkMapEntries; x += blockDim.x) ckMap[x] = 0xFFFFFFFFu;
     __syncthreads();
   }
-  const u64 tK1 = __builtin_readcyclecounter();       // BG_FINISH_TIMING
+  const u64 tK1 = __builtin_readcyclecounter();       // BG_DEBUG=finish
 
   // split traceback phases (linear checkpoint traceback only, BgFinishArgs::phase): WALK runs one
   // strip of a pair per workgroup (F.splitMap), the others one pair per workgroup
@@ -580,7 +580,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
   }
   const u64 tR1 = __builtin_amdgcn_s_memrealtime();  // this wave at the end-cell barrier
   __syncthreads();
-  const u64 tK2 = __builtin_readcyclecounter();       // BG_FINISH_TIMING: end cell known
+  const u64 tK2 = __builtin_readcyclecounter();       // BG_DEBUG=finish: end cell known
   if (F.dbg && (threadIdx.x & 63) == 0 && (threadIdx.x >> 6) < 2) {
     u64* d = F.dbg + (size_t)F.pairs[(ph == BG_PH_WALK) ? F.splitMap[blockIdx.x].x : blockIdx.x].index * 16;
     d[11 + 2 * (threadIdx.x >> 6)] = tR0;
@@ -721,7 +721,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     }
   };
   // decodes the 8x8 neighbourhood anchored at (k, l): lane (dk, dl) holds cell (k - dk, l - dl)
-  u64 tDec = 0, nDec = 0;                                // BG_FINISH_TIMING: decodes
+  u64 tDec = 0, nDec = 0;                                // BG_DEBUG=finish: decodes
   bool asyncPos = false;                                 // set below: post the walker's position
   auto reanchor = [&](int ka, int la) {
     k0 = ka; l0 = la;
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256) void bg_finish_kernel(BgFinishArgs F) {
     }
     if (tid == 0) { spl[SL.head + 8] = nt; spl[SL.head + 9] = preDone ? 1 : 0; }   // bg_split_stats
   }
-  u64 tJump = 0, tMiss = 0, nJump = 0, nMiss = 0, nRec = 0;   // BG_FINISH_TIMING instrumentation
+  u64 tJump = 0, tMiss = 0, nJump = 0, nMiss = 0, nRec = 0;   // BG_DEBUG=finish instrumentation
   u64 nSelf = 0;                                            // chunks the walker recomputed itself
   int lastReqS = -1, lastReqB = -1, sameReq = 0;            // barrier path: repeated requests
   const u64 tWalk0 = __builtin_readcyclecounter();

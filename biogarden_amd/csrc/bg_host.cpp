@@ -177,7 +177,7 @@ static const char* const kOptNames[BG_OPT_COUNT] = {
     "two_dp_streams", "wait_ms", "span"};
 
 // Host-side phases of prepare / fetch, accumulated per handle (bg_host_timing) and, with
-// BG_PREPARE_TIMING set, printed per call on stderr
+// BG_DEBUG=prepare, printed per call on stderr
 enum { kPhSync, kPhStage, kPhPlan, kPhAlloc, kPhUpload, kPhFetchWait, kPhFetchCopy, kPhFetchUnpack, kPhN };
 struct PhaseTimer {
   double* acc;
@@ -626,7 +626,7 @@ static int pipeline_phases(int S, int gw, int NC, int lag = 2) {
 // (one wave per SIMD, a lone wave issues fastest) in proportion to its cells, at most one wave
 // per strip and at most the CU count in all, so every group is resident at once.  R minimises
 // the slowest pair's pipeline: phases * 64 steps * the lone-wave step latency.  Measured on C3
-// (BG_DP_TIMING, conveyor step): ~48 + 10R cycles per step (the R-long v_max3 chain of a step
+// (BG_DEBUG=dp, conveyor step): ~48 + 10R cycles per step (the R-long v_max3 chain of a step
 // plus its DPP and two LDS reads), and an effective ~5 chunks per strip: a strip starts ~3.3
 // chunks after the one above (two for the anti-diagonal skew and the block, the rest hand-off),
 // and every caught-up consumer adds its hand-off latency to the pace of the strips below it.
@@ -719,9 +719,12 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
       cells += (uint64_t)n1[p] * n2[p];
     }
   if (comp.empty() || comp.size() * 4 > (size_t)h->cus || h->tuneW) return false;
-  // more than a handful of pairs: throughput over the strip chain's latency (plan_span), unless
-  // the SPAN kernel is switched off
-  if (comp.size() * 16 > (size_t)h->cus && h->o(BG_OPT_SPAN, -1) != 0) return false;
+  // more than cus / 8 pairs (M's 64- and 128-pair shares at 4 and 2 GPUs): the DP's throughput
+  // over the strip chain's latency (plan_span), unless the SPAN kernel is switched off.  At 32
+  // pairs the WIDE DP (0.97 ms) and SPAN's (1.07) are alike and WIDE's split traceback decides:
+  // 3 103 GCUPS against 2 843 (SPAN, split) and 1 969 (SPAN, one walker per pair;
+  // profiles/r06/shares)
+  if ((comp.size() * 8 > (size_t)h->cus && h->o(BG_OPT_SPAN, -1) != 0) || h->o(BG_OPT_SPAN, -1) == 1) return false;
   size_t maxn1 = 0;
   for (size_t p : comp) maxn1 = std::max(maxn1, n1[p]);
   if (maxn1 < 64 * 4 * 16) return false;                   // one workgroup's 16 waves suffice
@@ -1037,7 +1040,7 @@ static void plan_geometry(bg_aligner* h, size_t maxn1, size_t maxn2, size_t ncom
       T *= rounds;
       if (h->ack) {
         // the traceback recomputes the chunks its path crosses: per pair ~ (600 + 8R^2) cycles
-        // per row of walk and recomputation (BG_FINISH_TIMING, C2 / C5), with as many pairs in
+        // per row of walk and recomputation (BG_DEBUG=finish, C2 / C5), with as many pairs in
         // flight per CU as the finish workgroup's LDS allows
         const double fwg = std::max(1.0, std::floor(160.0 * 1024 / (double)std::max<size_t>(finLds, 1)));
         const double frounds = std::ceil((double)np / ((double)h->cus * fwg));
@@ -1379,7 +1382,12 @@ plan_again:
   h->splitInts = 0;
   {
     h->segc = std::max(1, h->o(BG_OPT_SPLIT_SEGMENT, BG_SPLIT_SEGC));
-    bool ok = h->wide && h->ckpt && !h->affine && !h->finFlags && mode != BG_LOCAL && h->o(BG_OPT_SPLIT, -1) != 0;
+    // SPAN batches only on request (BG_OPT_SPLIT = 1): at 64 and 128 pairs the split traceback's
+    // phases take longer than the one walker per pair they replace (128: 2.89 against 1.71 ms,
+    // 4 293 against 7 119 GCUPS; profiles/r06/shares)
+    const int osp = h->o(BG_OPT_SPLIT, -1);
+    bool ok = (h->wide || (h->span && osp == 1)) && h->ckpt && !h->affine && !h->finFlags && mode != BG_LOCAL &&
+              osp != 0;
     bool multi = false;
     for (const BgPair& P : h->plan) {
       if (P.n2 + 1 >= BG_SPLIT_SYM(R)) ok = false;
@@ -1686,7 +1694,7 @@ extern "C" int bg_batch_prepare_table(bg_aligner* h, int mode, size_t npairs,
 }
 
 namespace {
-// BG_EXEC_TIMING: the whole call, entry to return (stderr)
+// BG_DEBUG=exec: the whole call, entry to return (stderr)
 struct CallClock {
   const char* what;
   bool on;
@@ -1736,8 +1744,9 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   // only when no other execute's DP is still in flight (a lone alignment's wall, not a pipeline's
   // throughput: a second DP wants those CUs) — on either DP stream, so every slot's last DP is
   // asked; and only when the DP leaves a CU free
-  bool conc = h->split && h->splitConc == 1;
-  if (h->split && h->splitConc == 2) {
+  // (the concurrent pass reads WIDE's epoch-tagged granules: not SPAN)
+  bool conc = h->split && h->splitConc == 1 && h->wide;
+  if (h->split && h->splitConc == 2 && h->wide) {
     conc = h->shared() ? false : true;       // other handles' DPs are not visible here
     for (int x = 0; x < h->depth && conc; ++x) {
       if (!h->slot[x].inflight) continue;
@@ -1828,8 +1837,10 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   // workgroups fill the CUs beside the next DP as it is.
   // At pipeline depth 4 a WIDE batch's tracebacks rotate over three streams: a C3 walk (one
   // latency-bound workgroup, ~13 ms) then hides behind three DPs instead of two.
+  // SPAN batches (fewer pairs than CUs) alternate two: one walk of a 10 k x 10 k pair (~1.6 ms)
+  // is longer than their DP (1.1 ms at 64 pairs), and the walks of two executes fit side by side.
   int nfs = 1;
-  if (h->wide && !dbg_flags().finish)
+  if ((h->wide || h->span) && !dbg_flags().finish)
     nfs = h->wide ? std::min(3, std::max(2, h->depth - 1)) : 2;
   // the third stream is created on first use: HIP maps a process's streams onto 4 hardware
   // queues round-robin, and an extra stream per handle moves other handles' copies behind
@@ -1942,7 +1953,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     // GCUPS without it, tools/r04/prio_ab.sh); a WIDE batch's walks are its latency, and the
     // affine walks (recomputing with barriers) gain from it: MA 4 587 -> 4 714 GCUPS, C5 +0.9 %,
     // C2 even (tools/r05/prio_ab.sh).
-    if (!h->wide && !h->ack) F.flags |= BG_FIN_NOPRIO;
+    if (!h->wide && !h->span && !h->ack) F.flags |= BG_FIN_NOPRIO;
     if (dbg_flags().finish && h->dbgBuf.ensure(128 * (np + 1))) {
       F.dbg = h->dbgBuf.as<unsigned long long>();
       BG_HIP(hipMemsetAsync(h->dbgBuf.p, 0, 128 * np, fs));

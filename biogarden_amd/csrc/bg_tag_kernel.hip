@@ -360,7 +360,7 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
 #pragma unroll
       for (int k = 0; k <= R; ++k) { ckv[k] = 0; ckgv[k] = u32x2{0u, 0u}; }
       int Q = 0;
-      unsigned long long tData = 0, tFlow = 0;                   // BG_DP_TIMING: spin cycles
+      unsigned long long tData = 0, tFlow = 0;                   // BG_DEBUG=dp: spin cycles
       // LDS words read a boundary ahead (their latency hides behind the half's compute; the
       // words are monotonic, so a stale read only sends the wave down the polling path):
       // pc = the producer's half count, pv = the half after this boundary's (valid when pc says

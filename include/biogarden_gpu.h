@@ -346,7 +346,8 @@ enum {
   BG_OPT_FIN_SLOTS = 5,          /* recomputed-chunk slots of a traceback workgroup, 0 = all */
   BG_OPT_FIN_SYNC = 6,           /* 1: recomputation at a workgroup barrier (no helper waves) */
   BG_OPT_FIN_SELFSERVE = 7,      /* 1: the walker recomputes every chunk it misses itself */
-  BG_OPT_SPLIT = 8,              /* split traceback of few long pairs: 0 never (-1: automatic) */
+  BG_OPT_SPLIT = 8,              /* split traceback of few long pairs: 0 never, 1 also for SPAN
+                                    batches (-1: WIDE batches) */
   BG_OPT_SPLIT_SEGMENT = 9,      /* chunks per segment of the split traceback's exit pass */
   BG_OPT_SPLIT_CONCURRENT = 10,  /* the exit pass beside the DP: 0 never, 1 always (-1: when no
                                     other execute's DP is in flight) */

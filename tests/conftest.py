@@ -7,6 +7,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# torch ships its own HIP runtime (torch/lib/libamdhip64.so) and the library binds to whichever
+# libamdhip64 the process loaded first: import torch before any test loads libbiogarden_gpu.so,
+# or a later torch.cuda call finds no GPU (two runtimes in one process).  Importing initialises
+# no device.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 REF_FIX = os.path.join(GOLDEN, "reference_fixtures")
 

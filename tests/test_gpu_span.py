@@ -15,11 +15,12 @@ from parity_util import DNA, check_results, mutate, rand_seq, sample_indices
 pytestmark = pytest.mark.gpu
 
 
-def _run(mode, pairs, a, b, span, R=0, executes=1):
+def _run(mode, pairs, a, b, span, R=0, executes=1, split=None):
     from biogarden_amd import _native
     h = _native.Handle(0)
     try:
         h.set_option("span", span)
+        h.set_option("split", split)
         if R:
             h.set_tuning(R, 0)
         h.prepare(mode, pairs, _native.builtin_scoring(_native.BG_BLOSUM62), a, b)
@@ -48,8 +49,10 @@ def _pairs(seed, shapes, rate=0.12):
 def test_span_matches_one_workgroup_and_oracle(oracle, R):
     shapes = [(6000, 5000), (5200, 6100), (3000, 7000), (7000, 900), (4100, 4100), (2500, 2600)] * 3
     pairs = _pairs(100 + R, shapes)
-    got, st = _run("semiglobal", pairs, -1, -2, 1, R=R, executes=2)
+    got, st = _run("semiglobal", pairs, -1, -2, 1, R=R, executes=2, split=1 if R % 2 else None)
+    # the split traceback on request, at every other R
     assert st["wide"] == 2 and st["R"] == R and st["workgroups"] > len(pairs), st
+    assert st["split"] == (1 if R % 2 else 0), st
     ref, st0 = _run("semiglobal", pairs, -1, -2, 0, R=R)      # WIDE (lone waves) or one per pair
     assert st0["wide"] != 2, st0
     diff = [p for p in range(len(pairs)) if _key(got[p]) != _key(ref[p])]
@@ -60,13 +63,14 @@ def test_span_matches_one_workgroup_and_oracle(oracle, R):
 
 @pytest.mark.parametrize("mode,a,b", [("global", -2, -2), ("fitting", -1, -1), ("overlap", -1, -3),
                                       ("semiglobal", -3, -3)])
-def test_span_modes_vs_oracle(oracle, mode, a, b):
+@pytest.mark.parametrize("split", [None, 1])
+def test_span_modes_vs_oracle(oracle, mode, a, b, split):
     shapes = [(4000, 3500), (3900, 3000), (2000, 1500), (5000, 400), (64, 5000), (0, 300), (300, 0)]
     if mode == "fitting":
         shapes = [(4000, 3500), (3900, 3000), (2000, 1500), (5000, 400), (4500, 64), (0, 0), (300, 0)]
     pairs = _pairs(7 + len(mode) + a, shapes * 2)
-    got, st = _run(mode, pairs, a, b, 1, R=2)
-    assert st["wide"] == 2, st
+    got, st = _run(mode, pairs, a, b, 1, R=2, split=split)
+    assert st["wide"] == 2 and st["split"] == (1 if split == 1 else 0), st
     ref, _ = _run(mode, pairs, a, b, 0, R=2)
     assert [_key(r) for r in got] == [_key(r) for r in ref]
     check_results(oracle, mode, pairs, [_as_res(r) for r in got], "blosum62", a, b)
@@ -77,7 +81,7 @@ def test_span_planner_picks_groups_for_few_long_pairs():
     from tools import workloads as w
     pairs = w.metric_pairs(64, 10000, 10000, seed=w.SEED0 + 99)
     got, st = _run("semiglobal", pairs, -1, -2, -1)
-    assert st["wide"] == 2 and st["workgroups"] >= 2 * len(pairs), st
+    assert st["wide"] == 2 and st["workgroups"] >= 2 * len(pairs) and st["split"] == 0, st
     assert all(r["status"] == 0 for r in got)
 
 

@@ -65,7 +65,7 @@ def main():
                     help="also time N lone executes (execute + synchronize each): one alignment's wall")
     args = ap.parse_args()
     if args.timing:
-        os.environ["BG_FINISH_TIMING"] = "1"
+        os.environ["BG_DEBUG"] = "finish"
     if args.torch_init:                  # torch's HIP runtime state first, as in bench.py
         import torch
         torch.zeros(1, device="cuda")

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Per-wave strip timeline of the DP kernel for the first pair of a batch (BG_DP_TIMING).
+"""Per-wave strip timeline of the DP kernel for the first pair of a batch (BG_DEBUG=dp).
 
-    BG_DP_TIMING=1 python tools/dp_timeline.py [--pairs 256] [--len 10000] [--R 8 --waves 16]
+    BG_DEBUG=dp python tools/dp_timeline.py [--pairs 256] [--len 10000] [--R 8 --waves 16]
 
 One execute at pipeline depth 1 after a warm-up; the host prints, for each wave of pair 0, the
 strip it ran last in round 0, its start / first-chunk / end times and the cycles it spent waiting.

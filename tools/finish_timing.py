@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
-"""Per-pair cycle breakdown of the finish kernel (BG_FINISH_TIMING=1): walk total, jumper blocks,
+"""Per-pair cycle breakdown of the finish kernel (BG_DEBUG=finish): walk total, jumper blocks,
 misses (window loads / chunk recomputation), chunks recomputed.
     python tools/finish_timing.py [pairs] [ckpt 0/1] [R W]"""
 import os
 import sys
 
-os.environ["BG_FINISH_TIMING"] = "1"
+os.environ["BG_DEBUG"] = "finish"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from biogarden_amd import _native  # noqa: E402

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-strip table of a BG_DP_TIMING timeline (tools/dp_timeline.py output): start / end lags,
+"""Per-strip table of a BG_DEBUG=dp timeline (tools/dp_timeline.py output): start / end lags,
 durations and the split of waiting into data, flow-control and other (boundary) cycles."""
 import re
 import sys
