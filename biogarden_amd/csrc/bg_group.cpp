@@ -314,15 +314,18 @@ extern "C" int bg_group_collect(bg_group* g, bg_pair_result* res, uint8_t* out1,
   auto t = std::chrono::steady_clock::now();
   ++g->calls;
   const int M = (int)g->dev.size();
-  // 3 (second half): every member's wait and compact export (one host thread each)
-  std::vector<int> rc(M, BG_OK);
+  // 3 (second half): every member's compact export, queued without a host wait
+  // (bg_batch_export_compact_async) on its device's download stream behind the batch's traceback,
+  // into a buffer sized by the record's bound; the gather and the download below follow on the
+  // same streams, so the host waits once per collect, for the download
   std::vector<size_t> size(M, 0);
-  auto member = [&](int m) {
-    if (B.idx[m].empty()) return;
+  int err = BG_OK;
+  for (int m = 0; m < M && !err; ++m) {
+    if (B.idx[m].empty()) continue;
     const int x = kGSlots * m + B.slot;
     bg_aligner* h = g->h[x];
     size_t sz = 0;
-    int e = bg_batch_export_compact(h, nullptr, &sz);
+    int e = bg_batch_export_compact_bound(h, &sz);
     if (!e && g->ecap[x] < sz) {
       (void)hipSetDevice(g->dev[m]);
       if (g->ebuf[x]) (void)hipFree(g->ebuf[x]);
@@ -331,18 +334,10 @@ extern "C" int bg_group_collect(bg_group* g, bg_pair_result* res, uint8_t* out1,
       if (hipMalloc(&g->ebuf[x], sz + sz / 4) != hipSuccess) { g->ebuf[x] = nullptr; e = BG_E_NOMEM; }
       else g->ecap[x] = sz + sz / 4;
     }
-    if (!e) e = bg_batch_export_compact(h, g->ebuf[x], &sz);
+    if (!e) e = bg_batch_export_compact_async(h, g->ebuf[x], sz, g->cs[g->rankOf[m]]);
     size[m] = sz;
-    rc[m] = e;
-  };
-  {
-    std::vector<std::thread> th;
-    for (int m = 1; m < M; ++m) th.emplace_back(member, m);
-    member(0);
-    for (auto& x : th) x.join();
+    err = e;
   }
-  int err = BG_OK;
-  for (int m = 0; m < M && !err; ++m) err = rc[m];
   auto finish = [&](int e) {
     g->pending.pop_front();
     return e;
@@ -389,12 +384,9 @@ extern "C" int bg_group_collect(bg_group* g, bg_pair_result* res, uint8_t* out1,
     if (nr != ncclSuccess) return finish(nccl_fail(nr, "ncclSend / ncclRecv"));
     if (ne != ncclSuccess) return finish(nccl_fail(ne, "ncclGroupEnd"));
   }
-  for (size_t r = 1; r < g->cs.size(); ++r) {
-    if ((he = hipSetDevice(g->rankDev[r])) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
-    if ((he = hipStreamSynchronize(g->cs[r])) != hipSuccess) return finish(hip_fail(he, "gather (send side)"));
-  }
+  // (no host wait: the download below is queued behind the receives on the root's stream, and a
+  // sender's next export waits for its slot's readDone, which follows the send on that stream)
   if ((he = hipSetDevice(root)) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
-  if ((he = hipStreamSynchronize(g->cs[0])) != hipSuccess) return finish(hip_fail(he, "gather"));
   g->ms[kGGather] += ms_since(t);
   // 5: one download, then the expansion into the caller's buffers at the caller's offsets.  The
   // download is a kernel writing host-mapped pinned memory (bg_download_kernel), as the handles'
@@ -426,24 +418,24 @@ extern "C" int bg_group_collect(bg_group* g, bg_pair_result* res, uint8_t* out1,
       return finish(hip_fail(he, "download"));
   }
   g->ms[kGDownload] += ms_since(t);
+  // every member's record in one pass over the host pool (bgh::compact_expand_multi): the
+  // members' pairs are the work items, written at the caller's offsets
   const uint8_t* hb = static_cast<const uint8_t*>(g->hbuf);
-  for (int m = 0; m < M; ++m) {
-    const std::vector<size_t>& I = B.idx[m];
-    const size_t k = I.size();
-    if (!k) continue;
-    std::vector<const uint8_t*> p1(k), p2(k);
-    std::vector<size_t> l1(k), l2(k);
-    std::vector<uint64_t> dst(k);
-    for (size_t q = 0; q < k; ++q) {
-      p1[q] = B.s1[I[q]]; l1[q] = B.n1[I[q]];
-      p2[q] = B.s2[I[q]]; l2[q] = B.n2[I[q]];
-      dst[q] = B.coff[I[q]];
+  {
+    std::vector<bgh::CompactRec> recs;
+    std::vector<size_t> idx;
+    std::vector<uint64_t> dst;
+    idx.reserve(B.npairs);
+    dst.reserve(B.npairs);
+    for (int m = 0; m < M; ++m) {
+      const std::vector<size_t>& I = B.idx[m];
+      if (I.empty()) continue;
+      recs.push_back({hb + goff[m], size[m], I.size()});
+      for (size_t q : I) { idx.push_back(q); dst.push_back(B.coff[q]); }
     }
-    std::vector<bg_pair_result> rm(k);
-    const int e = bgh::compact_expand(hb + goff[m], size[m], k, p1.data(), l1.data(), p2.data(), l2.data(),
-                                      rm.data(), out1, out2, out_cap, dst.data());
+    const int e = bgh::compact_expand_multi(recs.data(), recs.size(), B.s1.data(), B.n1.data(), B.s2.data(),
+                                            B.n2.data(), idx.data(), res, out1, out2, out_cap, dst.data());
     if (e) return finish(e);
-    for (size_t q = 0; q < k; ++q) res[I[q]] = rm[q];
   }
   g->ms[kGExpand] += ms_since(t);
   return finish(BG_OK);

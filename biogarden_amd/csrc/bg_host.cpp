@@ -870,7 +870,7 @@ static double span_estimate(int S, int G, int W, int NC, int ops) {
 static bool plan_span(bg_aligner* h, const size_t* n1, const size_t* n2, size_t npairs, int* Rout,
                       int* Wout) {
   const int os = h->o(BG_OPT_SPAN, -1);
-  if (os == 0 || h->tuneW) return false;
+  if (os == 0 || (h->tuneW && os != 1)) return false;
   std::vector<size_t> comp;
   uint64_t cells = 0;
   for (size_t p = 0; p < npairs; ++p)
@@ -896,8 +896,9 @@ static bool plan_span(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
     const int fin = (h->depth > 1 && !relax) ? vgprs_of(fin_fn(h, Rc)) : 0;
     const int ops = 2 * Rc + 2;
     for (int Wc : {4, 8, 12, 16}) {
+      if (h->tuneW && Wc != h->tuneW) continue;
       const int wps = (Wc + 3) / 4;
-      if (wps * vg + fin > 512) continue;
+      if (wps * vg + fin > 512 && !h->tuneW) continue;
       if (640 + (size_t)Wc * bg_dp_tag_wave_lds_bytes(Rc) > 160 * 1024) continue;
       double T = 0.0, T1 = 0.0;
       int total = 0;
@@ -916,7 +917,10 @@ static bool plan_span(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
         T1 = std::max(T1, span_estimate(S, 1, Wc, NC, ops));
       }
       if (total > h->cus) continue;
-      if (T < best * 0.99 || (T < best * 1.01 && Rc > bestR)) {
+      // within 5 % the taller strips win: fewer instructions per cell than the model charges them
+      // (64 pairs: R = 10 / W = 4 ran 5 111 GCUPS against 4 788 for the estimate's R = 5 / W = 8,
+      // 2.7 % apart in the model; profiles/r06/span_sweep/)
+      if (T < best * 0.95 || (T < best * 1.05 && Rc > bestR)) {
         best = T; bestR = Rc; bestW = Wc; bestGroups = groups;
       }
       best1 = std::min(best1, T1);

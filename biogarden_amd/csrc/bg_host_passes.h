@@ -329,45 +329,68 @@ inline void unpack_strings(const std::vector<UnpackJob>& jobs, const uint8_t* h1
 // ---- the compact export record (include/biogarden_gpu.h bg_batch_export_compact) expanded on
 // the host into bg_batch_fetch's output, over the pool.  Every header is range-checked against
 // its pair before any byte is written; returns BG_OK or BG_E_ARG.
-// dstoff (np entries, or nullptr): where pair p's strings go in out1 / out2 (and its result's
-// offset); nullptr packs them back to back in pair order, as bg_batch_fetch does.
-inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uint8_t* const* s1,
-                          const size_t* n1, const uint8_t* const* s2, const size_t* n2,
-                          bg_pair_result* res, uint8_t* out1, uint8_t* out2, size_t out_cap,
-                          const uint64_t* dstoff = nullptr) {
-  if (!rec || bytes < 32 || (np && (!res || !n1 || !n2 || !s1 || !s2))) return BG_E_ARG;
-  uint64_t head[4];
-  std::memcpy(head, rec, 32);
-  if (head[0] != 0x31434742ull || head[1] != np || head[3] > 4) return BG_E_ARG;
-  const uint64_t opsBytes = head[2];
-  const bool semi = head[3] == 4;                      // bg_mode of the batch (BG_SEMIGLOBAL)
-  if (bytes < 32 + np * sizeof(bg_compact_hdr) + opsBytes) return BG_E_ARG;
-  const uint8_t* ops = rec + 32 + np * sizeof(bg_compact_hdr);
-  std::vector<bg_compact_hdr> hd(np);
-  if (np) std::memcpy(hd.data(), rec + 32, np * sizeof(bg_compact_hdr));
-  std::vector<uint64_t> off(np + 1, 0);
-  uint64_t end = 0;
-  for (size_t p = 0; p < np; ++p) {
-    off[p + 1] = off[p] + n1[p] + n2[p];
-    if (dstoff) off[p] = dstoff[p];
-    end = std::max<uint64_t>(end, off[p] + n1[p] + n2[p]);
-    if (dstoff && off[p] > (uint64_t)out_cap) return BG_E_ARG;
+// One or several records (bg_group: one per member) in ONE pass over the pool: the pairs of every
+// record are the work items, so a group's members expand side by side instead of one after the
+// other.  Record r covers rp[r] of the caller's pairs: s1 / n1 / s2 / n2 / res are indexed through
+// idx (nullptr: the records' pairs are 0, 1, 2, ... in order), dstoff[q] (nullptr: packed back to
+// back in that order, as bg_batch_fetch does) is where item q's strings go in out1 / out2.
+struct CompactRec {
+  const uint8_t* rec;
+  size_t bytes;
+  size_t np;
+};
+inline int compact_expand_multi(const CompactRec* recs, size_t nrec, const uint8_t* const* s1,
+                                const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                                const size_t* idx, bg_pair_result* res, uint8_t* out1, uint8_t* out2,
+                                size_t out_cap, const uint64_t* dstoff) {
+  struct Item {
+    bg_compact_hdr h;
+    const uint8_t* ops;     // the record's ops area
+    uint64_t opsBytes;
+    size_t p;               // caller pair
+    uint64_t off;           // output offset
+    bool semi;
+  };
+  size_t total = 0;
+  for (size_t r = 0; r < nrec; ++r) total += recs[r].np;
+  if (total && (!res || !n1 || !n2 || !s1 || !s2)) return BG_E_ARG;
+  std::vector<Item> it(total);
+  uint64_t end = 0, pos = 0;
+  size_t q = 0;
+  for (size_t r = 0; r < nrec; ++r) {
+    const CompactRec& R = recs[r];
+    if (!R.rec || R.bytes < 32) return BG_E_ARG;
+    uint64_t head[4];
+    std::memcpy(head, R.rec, 32);
+    if (head[0] != 0x31434742ull || head[1] != R.np || head[3] > 4) return BG_E_ARG;
+    if (R.bytes < 32 + R.np * sizeof(bg_compact_hdr) + head[2]) return BG_E_ARG;
+    const uint8_t* ops = R.rec + 32 + R.np * sizeof(bg_compact_hdr);
+    for (size_t k = 0; k < R.np; ++k, ++q) {
+      Item& I = it[q];
+      std::memcpy(&I.h, R.rec + 32 + k * sizeof(bg_compact_hdr), sizeof(bg_compact_hdr));
+      I.ops = ops;
+      I.opsBytes = head[2];
+      I.semi = head[3] == 4;                             // bg_mode of the batch (BG_SEMIGLOBAL)
+      I.p = idx ? idx[q] : q;
+      I.off = dstoff ? dstoff[q] : pos;
+      pos += n1[I.p] + n2[I.p];
+      end = std::max<uint64_t>(end, I.off + n1[I.p] + n2[I.p]);
+      if (dstoff && I.off > (uint64_t)out_cap) return BG_E_ARG;
+    }
   }
   if (end && (!out1 || !out2 || out_cap < end)) return BG_E_ARG;
   // every pair checked (over the pool) before any byte is written
   std::atomic<int> fail{BG_OK};
-  par_ranges(np, [&](size_t p) -> uint64_t { return hd[p].len / 4 + 64; }, [&](size_t lo, size_t hi) {
-  for (size_t p = lo; p < hi && fail.load(std::memory_order_relaxed) == BG_OK; ++p) {
-    const bg_compact_hdr& h = hd[p];
+  par_ranges(total, [&](size_t x) -> uint64_t { return it[x].h.len / 4 + 64; }, [&](size_t lo, size_t hi) {
+  for (size_t x = lo; x < hi && fail.load(std::memory_order_relaxed) == BG_OK; ++x) {
+    const bg_compact_hdr& h = it[x].h;
+    const size_t p = it[x].p;
     const uint64_t ncore = (uint64_t)h.len - h.npre - h.ntail;
-    auto bad = [&](int why) {
-      (void)why;
-      fail.store(BG_E_ARG, std::memory_order_relaxed);
-    };
-    if ((uint64_t)h.npre + h.ntail > h.len || h.len > n1[p] + n2[p] || h.ops_off + (ncore + 3) / 4 > opsBytes ||
+    auto bad = [&]() { fail.store(BG_E_ARG, std::memory_order_relaxed); };
+    if ((uint64_t)h.npre + h.ntail > h.len || h.len > n1[p] + n2[p] || h.ops_off + (ncore + 3) / 4 > it[x].opsBytes ||
         h.start1 > n1[p] || h.start2 > n2[p] || h.end_i > n1[p] || h.end_j > n2[p] ||
         (n1[p] && !s1[p]) || (n2[p] && !s2[p])) {
-      bad(1);
+      bad();
       continue;
     }
     // the core consumes exactly s1[start1, end_i) and s2[start2, end_j): op 0 (diagonal) takes
@@ -375,32 +398,32 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
     // the ops' low and high bit planes
     uint64_t c1 = 0, c2 = 0;
     bool three = false;
-    const uint8_t* po = ops + h.ops_off;
+    const uint8_t* po = it[x].ops + h.ops_off;
     const uint64_t kLo = 0x5555555555555555ull;
-    uint64_t x = 0;
-    for (; x + 32 <= ncore; x += 32) {
+    uint64_t y = 0;
+    for (; y + 32 <= ncore; y += 32) {
       uint64_t w;
-      std::memcpy(&w, po + x / 4, 8);
+      std::memcpy(&w, po + y / 4, 8);
       const uint64_t lo = w & kLo, hi = (w >> 1) & kLo;
       three |= (lo & hi) != 0;
       c1 += 32 - (uint64_t)__builtin_popcountll(hi);
       c2 += 32 - (uint64_t)__builtin_popcountll(lo);
     }
-    for (; x < ncore; ++x) {
-      const int op = (po[x / 4] >> (2 * (x % 4))) & 3;
+    for (; y < ncore; ++y) {
+      const int op = (po[y / 4] >> (2 * (y % 4))) & 3;
       three |= op == 3;
       c1 += op != 2;
       c2 += op != 1;
     }
-    if (three) { bad(2); continue; }
-    if (h.start1 + c1 != h.end_i || h.start2 + c2 != h.end_j) { bad(3); continue; }
+    if (three) { bad(); continue; }
+    if (h.start1 + c1 != h.end_i || h.start2 + c2 != h.end_j) { bad(); continue; }
     // the reference's semiglobal assembly (aligner.rs:389-428): the tail gap columns run from the
     // end cell to the last row / column, and a walk that returned (status 0) is preceded by the
     // prefix of the sequence it stopped in, exactly up to its start cell (row case: s2[0, start2),
     // column case: s1[0, start1)); the other modes have neither
     const bool colcase = h.end_i < n1[p];
-    if (!semi) {
-      if (h.npre || h.ntail) bad(4);
+    if (!it[x].semi) {
+      if (h.npre || h.ntail) bad();
     } else {
       const uint64_t tail = colcase ? n1[p] - h.end_i : n2[p] - h.end_j;
       const uint64_t pre = colcase ? h.start1 : h.start2;
@@ -409,40 +432,77 @@ inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uin
       const bool whole = h.npre == pre && h.ntail == tail;
       const bool stopped = h.npre == 0 && (h.ntail == 0 || h.ntail == tail);
       if (h.status == 0 ? !whole : h.status == BG_REF_DIVERGENT ? !(whole || stopped) : !stopped)
-        bad(5);
+        bad();
     }
   }
   });
   if (fail.load() != BG_OK) return fail.load();
-  par_ranges(np, [&](size_t p) -> uint64_t { return 2ull * hd[p].len + 64; }, [&](size_t lo, size_t hi) {
-    for (size_t p = lo; p < hi; ++p) {
-      const bg_compact_hdr& h = hd[p];
+  par_ranges(total, [&](size_t x) -> uint64_t { return 2ull * it[x].h.len + 64; }, [&](size_t lo, size_t hi) {
+    for (size_t x = lo; x < hi; ++x) {
+      const bg_compact_hdr& h = it[x].h;
+      const size_t p = it[x].p;
       bg_pair_result& o = res[p];
       std::memset(&o, 0, sizeof(o));
-      o.status = h.status; o.score = h.score; o.offset = off[p]; o.len = h.len;
+      o.status = h.status; o.score = h.score; o.offset = it[x].off; o.len = h.len;
       o.end_i = h.end_i; o.end_j = h.end_j; o.start1 = h.start1; o.start2 = h.start2;
-      uint8_t* a1 = out1 + off[p];
-      uint8_t* a2 = out2 + off[p];
+      uint8_t* a1 = out1 + it[x].off;
+      uint8_t* a2 = out2 + it[x].off;
+      const uint8_t* r1 = s1[p];
+      const uint8_t* r2 = s2[p];
       const bool colcase = h.end_i < n1[p];
-      uint64_t x = 0;
-      for (uint32_t q = 0; q < h.npre; ++q, ++x) {
-        a1[x] = colcase ? s1[p][q] : (uint8_t)'-';
-        a2[x] = colcase ? (uint8_t)'-' : s2[p][q];
+      uint64_t y = 0;
+      if (h.npre) {
+        if (colcase) { std::memcpy(a1, r1, h.npre); std::memset(a2, '-', h.npre); }
+        else { std::memset(a1, '-', h.npre); std::memcpy(a2, r2, h.npre); }
+        y = h.npre;
       }
       const uint64_t ncore = (uint64_t)h.len - h.npre - h.ntail;
+      const uint8_t* po = it[x].ops + h.ops_off;
       size_t i = h.start1, j = h.start2;
-      for (uint64_t q = 0; q < ncore; ++q, ++x) {
-        const int op = (ops[h.ops_off + q / 4] >> (2 * (q % 4))) & 3;
-        a1[x] = op != 2 ? s1[p][i++] : (uint8_t)'-';
-        a2[x] = op != 1 ? s2[p][j++] : (uint8_t)'-';
+      // four columns per ops byte: diagonal bytes (0x00, the common case) copy four residues of
+      // each sequence, the others go column by column
+      uint64_t q0 = 0;
+      for (; q0 + 4 <= ncore; q0 += 4, y += 4) {
+        const uint8_t ob = po[q0 / 4];
+        if (ob == 0) {
+          std::memcpy(a1 + y, r1 + i, 4);
+          std::memcpy(a2 + y, r2 + j, 4);
+          i += 4;
+          j += 4;
+          continue;
+        }
+        for (int k = 0; k < 4; ++k) {
+          const int op = (ob >> (2 * k)) & 3;
+          a1[y + k] = op != 2 ? r1[i] : (uint8_t)'-';
+          a2[y + k] = op != 1 ? r2[j] : (uint8_t)'-';
+          i += op != 2;
+          j += op != 1;
+        }
       }
-      for (uint32_t q = 0; q < h.ntail; ++q, ++x) {
-        a1[x] = colcase ? s1[p][h.end_i + q] : (uint8_t)'-';
-        a2[x] = colcase ? (uint8_t)'-' : s2[p][h.end_j + q];
+      for (; q0 < ncore; ++q0, ++y) {
+        const int op = (po[q0 / 4] >> (2 * (q0 % 4))) & 3;
+        a1[y] = op != 2 ? r1[i] : (uint8_t)'-';
+        a2[y] = op != 1 ? r2[j] : (uint8_t)'-';
+        i += op != 2;
+        j += op != 1;
+      }
+      if (h.ntail) {
+        if (colcase) { std::memcpy(a1 + y, r1 + h.end_i, h.ntail); std::memset(a2 + y, '-', h.ntail); }
+        else { std::memset(a1 + y, '-', h.ntail); std::memcpy(a2 + y, r2 + h.end_j, h.ntail); }
       }
     }
   });
   return BG_OK;
+}
+
+// One record of np pairs (pairs 0 .. np-1 of the arrays); dstoff as above.
+inline int compact_expand(const uint8_t* rec, size_t bytes, size_t np, const uint8_t* const* s1,
+                          const size_t* n1, const uint8_t* const* s2, const size_t* n2,
+                          bg_pair_result* res, uint8_t* out1, uint8_t* out2, size_t out_cap,
+                          const uint64_t* dstoff = nullptr) {
+  if (!rec || bytes < 32 || (np && (!res || !n1 || !n2 || !s1 || !s2))) return BG_E_ARG;
+  const CompactRec R{rec, bytes, np};
+  return compact_expand_multi(&R, 1, s1, n1, s2, n2, nullptr, res, out1, out2, out_cap, dstoff);
 }
 
 }  // namespace bgh
