@@ -659,6 +659,10 @@ def main():
     if backend == "nccl" and n_devices != world:
         print("bench.py: %d ranks ran on %d distinct GPUs" % (world, n_devices), file=sys.stderr)
         sys.exit(3)
+    if n_devices < world:
+        # ranks sharing a GPU (the gloo rehearsal): WIDE and SPAN DPs spin on workgroups of their
+        # own grid, and two processes' grids on one GPU could each hold part of the CUs forever
+        os.environ["BG_OPTIONS"] = ",".join(x for x in (os.environ.get("BG_OPTIONS", ""), "span=0,wide=0") if x)
 
     from biogarden_amd import _native
 
@@ -871,6 +875,7 @@ def main():
                                                  "step" if strong_head
                                                  else "independent pairs per rank")},
         "devices": sorted(set("%s/%s" % d for d in everyone)),
+        "rehearsal": None if n_devices == world else "ranks share %d GPU(s): WIDE / SPAN plans off" % n_devices,
         "collectives": backend if world > 1 else None,
         "roofline": roof,
         "steady_state": steady,

@@ -35,7 +35,7 @@ EXPORTS = ["bg_scoring_builtin", "bg_aligner_new", "bg_aligner_free", "bg_align"
 # bg_set_option keys (include/biogarden_gpu.h BG_OPT_*), by their BG_OPTIONS names
 OPTIONS = ("grouped", "group_pairs", "group_waves", "wide_waves", "fin_waves", "fin_slots",
            "fin_sync", "fin_selfserve", "split", "split_segment", "split_concurrent",
-           "split_wait_ms", "two_dp_streams", "wait_ms", "span")
+           "split_wait_ms", "two_dp_streams", "wait_ms", "span", "wide")
 
 
 class NativeUnavailable(RuntimeError):

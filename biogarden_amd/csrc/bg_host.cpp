@@ -174,7 +174,7 @@ static const BgDebug& dbg_flags() {
 static const char* const kOptNames[BG_OPT_COUNT] = {
     "grouped", "group_pairs", "group_waves", "wide_waves", "fin_waves", "fin_slots", "fin_sync",
     "fin_selfserve", "split", "split_segment", "split_concurrent", "split_wait_ms",
-    "two_dp_streams", "wait_ms", "span"};
+    "two_dp_streams", "wait_ms", "span", "wide"};
 
 // Host-side phases of prepare / fetch, accumulated per handle (bg_host_timing) and, with
 // BG_DEBUG=prepare, printed per call on stderr
@@ -718,7 +718,7 @@ static bool plan_wide(bg_aligner* h, const size_t* n1, const size_t* n2, size_t 
       comp.push_back(p);
       cells += (uint64_t)n1[p] * n2[p];
     }
-  if (comp.empty() || comp.size() * 4 > (size_t)h->cus || h->tuneW) return false;
+  if (comp.empty() || comp.size() * 4 > (size_t)h->cus || h->tuneW || h->o(BG_OPT_WIDE, -1) == 0) return false;
   // more than cus / 8 pairs (M's 64- and 128-pair shares at 4 and 2 GPUs): the DP's throughput
   // over the strip chain's latency (plan_span), unless the SPAN kernel is switched off.  At 32
   // pairs the WIDE DP (0.97 ms) and SPAN's (1.07) are alike and WIDE's split traceback decides:

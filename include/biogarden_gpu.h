@@ -359,7 +359,11 @@ enum {
   BG_OPT_SPAN = 14,              /* fewer pairs than CUs: each pair over a group of many-wave
                                     workgroups: 0 never, 1 whenever it applies (-1: when the
                                     planner's estimate gains) */
-  BG_OPT_COUNT = 15
+  BG_OPT_WIDE = 15,              /* 0: never WIDE (few long pairs over lone-wave workgroups).
+                                    WIDE and SPAN DPs spin on workgroups of their own grid, so all
+                                    of a grid's workgroups must be resident at once: processes
+                                    sharing one GPU should turn both off */
+  BG_OPT_COUNT = 16
 };
 int bg_set_option(bg_aligner* h, int key, int value);
 int bg_get_option(bg_aligner* h, int key, int* value);
