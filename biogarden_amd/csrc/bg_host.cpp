@@ -1698,6 +1698,8 @@ extern "C" int bg_batch_prepare_table(bg_aligner* h, int mode, size_t npairs,
 }
 
 namespace {
+// BG_DEBUG=dp: 8 words per wave, then 32 words of conveyor boundary times per wave
+constexpr size_t kDpDbgBytes = 8 * 4096 * (8 + 32);
 // BG_DEBUG=exec: the whole call, entry to return (stderr)
 struct CallClock {
   const char* what;
@@ -1792,9 +1794,9 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
     A.wgmap = h->wgmapBuf.as<int2>();
     A.gprog = (h->wide || h->span) ? S.gprog.as<uint32_t>() : h->gprogBuf.as<uint32_t>();
     A.dbg = nullptr;
-    if (dbg_flags().dp && h->tag && h->dpDbg.ensure(64 * 4096)) {
+    if (dbg_flags().dp && h->tag && h->dpDbg.ensure(kDpDbgBytes)) {
       A.dbg = h->dpDbg.as<unsigned long long>();
-      BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, 64 * 4096, ds));
+      BG_HIP(hipMemsetAsync(h->dpDbg.p, 0, kDpDbgBytes, ds));
     }
     if (h->wide || h->span) BG_HIP(hipMemsetAsync(S.gprog.p, 0, 4 * ((size_t)h->progWords + 8), ds));
     if (conc) {
@@ -2111,8 +2113,8 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
     // first pair's waves: strip start / chunk-0 end / strip end relative to the earliest start
     // (s_memrealtime, 100 MHz, one clock for every XCD), and the shader cycles each wave spent
     // polling for the strip above out of its whole strip (s_memtime)
-    std::vector<unsigned long long> d(8 * 4096);
-    BG_HIP(hipMemcpy(d.data(), h->dpDbg.p, 64 * 4096, hipMemcpyDeviceToHost));
+    std::vector<unsigned long long> d(kDpDbgBytes / 8);
+    BG_HIP(hipMemcpy(d.data(), h->dpDbg.p, kDpDbgBytes, hipMemcpyDeviceToHost));
     unsigned long long t0 = ~0ull, tend = 0;
     int nrec = 0;
     for (int g = 0; g < 4096; ++g)
@@ -2126,6 +2128,27 @@ extern "C" int bg_batch_fetch(bg_aligner* h, bg_pair_result* res, uint8_t* out1,
                    d[8 * g], (d[8 * g + 1] - t0) * 0.01, (d[8 * g + 2] - t0) * 0.01,
                    (d[8 * g + 3] - t0) * 0.01, (double)d[8 * g + 4], (double)d[8 * g + 5],
                    (double)d[8 * g + 6], (double)d[8 * g + 7]);
+    }
+    // conveyor strips: the first twelve half boundaries and two steady ones (g = 1000, 1003),
+    // arrival / departure in us from t0, and the departure behind the producer's at g + 3
+    const unsigned long long* bt = d.data() + 8 * 4096;
+    for (int g = 0; g < 4096; ++g) {
+      const unsigned long long* q = bt + 32 * g;
+      if (!q[1]) continue;
+      if (!(g < 10 || (g >= 64 && g < 68) || (g >= 128 && g < 132) || (g >= 256 && g < 260))) continue;
+      std::fprintf(stderr, "  bnd wave %4d:", g);
+      for (int x = 0; x < 14; ++x) {
+        if (!q[2 * x + 1]) { std::fprintf(stderr, "     -     "); continue; }
+        std::fprintf(stderr, " %6.2f/%6.2f", (q[2 * x] - t0) * 0.01, (q[2 * x + 1] - t0) * 0.01);
+      }
+      std::fprintf(stderr, "\n");
+      if (g > 0 && bt[32 * (g - 1) + 1]) {
+        const unsigned long long* p = bt + 32 * (g - 1);
+        std::fprintf(stderr, "  lag  wave %4d:", g);
+        for (int x = 0; x + 3 < 12; ++x)
+          std::fprintf(stderr, " %6.2f", q[2 * x + 1] && p[2 * (x + 3) + 1] ? ((double)q[2 * x + 1] - (double)p[2 * (x + 3) + 1]) * 0.01 : 0.0);
+        std::fprintf(stderr, "  steady %6.2f\n", q[25] && p[27] ? ((double)q[25] - (double)p[27]) * 0.01 : 0.0);
+      }
     }
   }
   if (dbg_flags().finish && h->dbgBuf.p && np) {

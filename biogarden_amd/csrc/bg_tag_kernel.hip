@@ -36,6 +36,7 @@
 
 #include "bg_dev_util.h"
 #include "bg_tag_common.h"
+#include "bg_score_step.h"
 
 using namespace bgk;
 
@@ -106,9 +107,24 @@ __device__ __forceinline__ void poll_pause(int& n) {
   else poll_backoff(n);
 }
 
+// profile entries per wave: the four DNA codes and (checkpoint mode) the border code, every byte
+// -128, that the code row holds outside seq2 (columns j <= 0 and j > n2): there the diagonal
+// candidate never wins, so
+//   * beyond n2 every cell repeats its row's column n2: M'(i, j) = max(M'(i-1, j), M'(i, j-1)) and
+//     M'(i, n2) >= M'(i-1, n2) in the frame.  A strip's registers end holding M(i, n2), stored
+//     once, instead of a per-step catch in its last chunks;
+//   * before column 0, with the border values M'(i, 0) non-decreasing from 0 (every mode but
+//     global, a <= 0; global with a == b), the lanes' column-0 values loaded at the strip's start
+//     survive the steps before each lane reaches column 0: chunk 0 needs no per-step reset.
+// The row above of strip 0 is row 0 clamped at column n2, so that it freezes too.
+// The last chunk's row above (block NC - 1, beyond n2 for lane 0) is never handed down: the strip
+// above finishes before it is final.  Stale there, it would break the freeze, so a consumer takes
+// kRowAboveNone for it (the row above then never wins past n2 either).
+constexpr int kTagCodes = 5;
+constexpr int kRowAboveNone = -(1 << 29);
 template <int R>
 __host__ __device__ constexpr int tag_wave_ints() {
-  return kTagWaveInts + 4 * 64 * ProfW<R>::v + kTagStageU16 / 2 + kMailSlots * 64;
+  return kTagWaveInts + kTagCodes * 64 * ProfW<R>::v + kTagStageU16 / 2 + kMailSlots * 64;
 }
 
 // CKPT: the score-only forward pass of the checkpoint traceback (score_chunk, untagged M'
@@ -153,7 +169,7 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
     const uint8_t* g = A.codes2 + Pp.off2;
     const int n = (Pp.nc + 2) * BG_CHUNK;
     for (int x = (int)threadIdx.x - 64; x < n; x += blockDim.x)
-      sRow[x] = (x >= 0 && x < Pp.n2) ? (uint16_t)(g[x] * (32 * RW)) : (uint16_t)0;
+      sRow[x] = (x >= 0 && x < Pp.n2) ? (uint16_t)(g[x] * (32 * RW)) : (uint16_t)(CKPT ? 4 * 256 * RW : 0);
   } else if (WIDE && A.codes_in_lds == 2) {
     const BgPair& Pp = A.pairs[pairIdx];
     const uint8_t* g = A.codes2 + Pp.off2;   // code * 8
@@ -194,11 +210,11 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
   const size_t stripDw = (size_t)NC * (BG_CHUNK / BG_TRACE_BLK) * R * 2 * BG_WAVE;
   int* waveLds = reinterpret_cast<int*>(smem + A.aux_lds_off) + w * tag_wave_ints<R>();
   int* profTab = waveLds + kTagWaveInts;
-  uint16_t* stage = reinterpret_cast<uint16_t*>(profTab + 4 * 64 * RW);
-  int* mailbox = profTab + 4 * 64 * RW + kTagStageU16 / 2;   // this wave's outgoing blocks
+  uint16_t* stage = reinterpret_cast<uint16_t*>(profTab + kTagCodes * 64 * RW);
+  int* mailbox = profTab + kTagCodes * 64 * RW + kTagStageU16 / 2;   // this wave's outgoing blocks
   const int prevW = (w + W - 1) % W;                         // producer wave of the strip above
   int* prevMail = reinterpret_cast<int*>(smem + A.aux_lds_off) + prevW * tag_wave_ints<R>() +
-                  (kTagWaveInts + 4 * 64 * RW + kTagStageU16 / 2);
+                  (kTagWaveInts + kTagCodes * 64 * RW + kTagStageU16 / 2);
 
   TagCtx C;
   C.a = a; C.b = b; C.mode = mode; C.n1 = n1; C.n2 = n2; C.lane = lane;
@@ -213,6 +229,10 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
 
   const uint8_t* c1 = A.codes1 + P.off1;
   const uint8_t* g2 = A.codes2 + P.off2;  // code * 8 (DNA path)
+  // the staged code of a column outside seq2: the border entry (checkpoint mode), else code 0
+  constexpr uint16_t kBorder = CKPT ? 4 * 256 * RW : 0;
+  // checkpoint mode: chunk 0 without a column-0 reset (see kTagCodes)
+  const bool colMono = CKPT && a <= 0 && (mode != BGK_GLOBAL || a == b);
   // raw codes of columns t0-64+lane+64q, q = 0..2 (clamped, unconditional loads: they are only
   // consumed at the next chunk's start, so their latency hides behind a whole chunk)
   auto fetch_codes = [&](int c, int (&v)[3]) {
@@ -227,7 +247,7 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const int x = c * BG_CHUNK - 64 + lane + 64 * q;
-      stage[lane + 64 * q] = (uint16_t)(((unsigned)x < (unsigned)n2) ? v[q] * (32 * RW) : 0);
+      stage[lane + 64 * q] = (uint16_t)(((unsigned)x < (unsigned)n2) ? v[q] * (32 * RW) : kBorder);
     }
   };
   // ... or from the packed row in LDS (columns t0 - 64 + lane + 64q: byte 16(c + q) + lane / 4)
@@ -235,7 +255,8 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       const unsigned v = sPk[16 * (c + q) + (lane >> 2)];
-      stage[lane + 64 * q] = (uint16_t)(((v >> (2 * (lane & 3))) & 3u) * (256 * RW));
+      const int x = c * BG_CHUNK - 64 + lane + 64 * q;
+      stage[lane + 64 * q] = (uint16_t)(((unsigned)x < (unsigned)n2) ? ((v >> (2 * (lane & 3))) & 3u) * (256 * RW) : kBorder);
     }
   };
 
@@ -295,6 +316,10 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
           if (wd * 4 + bb < R) v |= (((unsigned)pk[wd * 4 + bb] >> (8 * cd)) & 0xffu) << (8 * bb);
         profTab[(cd * 64 + lane) * RW + wd] = (int)v;
       }
+    if constexpr (CKPT) {
+#pragma unroll
+      for (int wd = 0; wd < RW; ++wd) profTab[(4 * 64 + lane) * RW + wd] = (int)0x80808080;   // border
+    }
     S.topPrev = 0; S.Xlast = CKPT ? 0 : 2;
     int32_t* ckBase = CKPT ? reinterpret_cast<int32_t*>(A.trace + P.trace_off / 4) +
                                  (size_t)s * NC * (R + 1) * BG_WAVE + lane
@@ -406,9 +431,11 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
         // the previous boundary's store data stays allocated until here
         asm volatile("" ::"v"(kv), "v"(kg.x), "v"(kg.y));
         const unsigned long long tw0 = dbgOn ? __builtin_amdgcn_s_memtime() : 0;
+        const unsigned long long tw0r =
+            (dbgOn && (g < 12 || g == 1000 || g == 1003)) ? __builtin_amdgcn_s_memrealtime() : 0;
         int inV;
         if constexpr (IN == 0) {
-          const int j = 32 * g + l32;
+          const int j = min(32 * g + l32, n2);                             // frozen past n2
           inV = wadd(row0_M(mode, j, a, b), -wmul(a, j));                    // M'(0, j)
         } else if constexpr (IN == 1) {
           const int sq = hb + g;
@@ -421,7 +448,7 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             pv = prevMail[(sq % KH) * 32 + l32];
           }
-          inV = pv;
+          inV = g < nh ? pv : kRowAboveNone;                             // past the last block: frozen
           __atomic_signal_fence(__ATOMIC_SEQ_CST);              // LDS: the release after the read
           if (lane == 0) __hip_atomic_store(sCons + w, sq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -438,13 +465,22 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
             }
             if (dbgOn) tData += __builtin_amdgcn_s_memtime() - td0;
           }
-          inV = (int)gv.x;
+          inV = g < nh ? (int)gv.x : kRowAboveNone;                       // past the last block: frozen
           if (g + 2 < nh) gv = __builtin_amdgcn_raw_buffer_load_b64(rGi, vH8, (g + 2) * 256, kSC1);
         }
         const int Qo = Q;
         Q = lo ? inV : Q;
         if (g >= 3) emit(g - 3, Qo);
-        if (dbgOn) tWait += __builtin_amdgcn_s_memtime() - tw0;
+        if (dbgOn) {
+          tWait += __builtin_amdgcn_s_memtime() - tw0;
+          // BG_DEBUG=dp: the first boundaries' and two steady ones' (1000, 1003) arrival / departure
+          // (s_memrealtime), [g][arrive, depart] after the 8-word records
+          const int gs = g < 12 ? g : (g == 1000 ? 12 : (g == 1003 ? 13 : -1));
+          if (gs >= 0 && lane == 0) {
+            A.dbg[8 * 4096 + gw * 32 + 2 * gs] = tw0r;
+            A.dbg[8 * 4096 + gw * 32 + 2 * gs + 1] = __builtin_amdgcn_s_memrealtime();
+          }
+        }
       };
       for (int c = 0; c < NC; ++c) {
         if (dbgOn && c == 1 && lane == 0) A.dbg[gw * 8 + 2] = __builtin_amdgcn_s_memrealtime();
@@ -480,8 +516,7 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
           for (int k = 0; k <= R; ++k) asm volatile("" ::"v"(ckv[k]), "v"(ckgv[k].x), "v"(ckgv[k].y));
           boundary(2 * c + 1, gvB);
         };
-        const bool edge = (c == 0) || (c * BG_CHUNK + BG_CHUNK - 1 >= n2);
-        if (edge) score_chunk_conv<R, TV_EDGE>(S, C, c, Q, mid);
+        if (c == 0 && !colMono) score_chunk_conv<R, TV_COL0>(S, C, c, Q, mid);
         else score_chunk_conv<R, TV_FAST>(S, C, c, Q, mid);
       }
       if (nh >= 1) emit(nh - 1, Q);                              // the last half: 2 NC - 3
@@ -546,7 +581,8 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
       const int hseq = rho * nh + 2 * c;                         // CONV mode: its first half
       const int jb = c * BG_CHUNK + lane;
       if (s == 0) {
-        const int m0 = wadd(row0_M(mode, jb, a, b), -wmul(a, jb));          // M'(0, j)
+        const int jr = CKPT ? min(jb, n2) : jb;                            // frozen past n2
+        const int m0 = wadd(row0_M(mode, jr, a, b), -wmul(a, jr));          // M'(0, j)
         waveLds[lane] = CKPT ? m0 : 4 * m0 + 2;                             // (X form)
         C.bIn = waveLds;
       } else if (hbmAhead && CONVMODE) {
@@ -599,6 +635,10 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
           C.bIn = waveLds;
         }
       }
+      if (CKPT && s > 0 && c >= nblk) {                            // never handed down: frozen
+        waveLds[lane] = kRowAboveNone;
+        C.bIn = waveLds;
+      }
       // the block this chunk finishes (c-1) goes to mailbox slot (seq-1) mod 4 once the
       // consumer has finished the chunk that read that slot last (sequence seq-1-4)
       C.mail = nullptr;
@@ -624,9 +664,9 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
                                ((unsigned long long)A.epoch << 32) | (uint32_t)(k < R ? S.Y[k] : S.topPrev),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
-        if (edge) score_chunk<R, TV_EDGE, LONE, false, WIDE>(S, C, c);
+        if (c == 0 && !colMono) score_chunk<R, TV_COL0, LONE, false, WIDE>(S, C, c);
         else if (lastStrip && selRow) score_chunk<R, TV_SEL, LONE, false, WIDE>(S, C, c);
-        else if (R <= 4 && s == 0) {
+        else if (R <= 4 && s == 0 && !edge) {
           // row 0 above: M'(0, j) for j >= 1 is linear (semiglobal / local / overlap: M = 0;
           // global / fitting: a + (j - 1) b)
           const bool flat = mode == BGK_SEMIGLOBAL || mode == BGK_LOCAL || mode == BGK_OVERLAP;
@@ -670,6 +710,17 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
       if (mailIn && lane == 0)   // release: this chunk's reads of the slot(s) are done
         __hip_atomic_store(sCons + w, CONVMODE ? hseq + 2 : seq + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    }
+    if constexpr (CKPT) {
+      // M(i, n2): past column n2 every cell repeats it (the border code), so the strip's registers
+      // end holding the lane's column n2 (every lane passes it: NC = n2 / 64 + 2 chunks)
+      if (n2 > 0) {
+#pragma unroll
+        for (int k = 0; k < R; ++k) {
+          const int i = C.rowbase + k + 1;
+          if (i <= n1) C.lastcol[i] = wadd(S.Y[k], wmul(a, i + n2));
+        }
+      }
     }
     if (dbgOn && lane == 0) {
       A.dbg[gw * 8 + 0] = (unsigned long long)s;
