@@ -4,6 +4,11 @@
 #pragma once
 #include "bg_tag_common.h"
 
+// operand pipeline depth of the many-wave score step (A/B builds: -DBG_PF_MANY=2)
+#ifndef BG_PF_MANY
+#define BG_PF_MANY 1
+#endif
+
 namespace bgk {
 
 // Score-only forward step (checkpoint mode): values are the untagged M'(i,j) = M(i,j) - a(i+j),
@@ -26,7 +31,7 @@ __device__ __forceinline__ void score_chunk(TagStrip<R>& S, const TagCtx& C, int
   // flight while a step computes.  One step hides the LDS latency at several waves per SIMD; a
   // lone wave per SIMD (WIDE) issues a step in a few tens of cycles, so it runs 4 steps ahead
   // (rotating registers; 32 % PF == 0 keeps the rotation aligned across the two 32-step halves).
-  constexpr int PF = WIDE ? 4 : 1;
+  constexpr int PF = WIDE ? 4 : BG_PF_MANY;
   int c0v[R];                                                // TV_COL0: this lane's M'(i, 0)
   if constexpr (VAR == TV_COL0) {
 #pragma unroll

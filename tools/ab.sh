@@ -1,4 +1,4 @@
-# A/B of library builds on the GPU box: the tree's libbiogarden_gpu.so against exp/<name>.so, in
+# A/B of library builds on the GPU box: the tree's libbiogarden_gpu.so against variants/<name>.so, in
 # two interleaved passes (drift control).  usage: LIBS="a b" WHAT="M C3 C2" bash tools/ab.sh
 #   M   bench.py metric leg only (no CPU / h2h / affine / configs legs)
 #   MA  bench.py's affine leg's workload as the headline (--open -11 --extend -1)
@@ -16,7 +16,7 @@ run_one() {   # $1 variant, $2 what
 }
 for pass in 1 2; do
   for v in tree $LIBS; do
-    if [ $v = tree ]; then cp /tmp/lib_tree.so biogarden_amd/libbiogarden_gpu.so; else cp exp/$v.so biogarden_amd/libbiogarden_gpu.so; fi
+    if [ $v = tree ]; then cp /tmp/lib_tree.so biogarden_amd/libbiogarden_gpu.so; else cp variants/$v.so biogarden_amd/libbiogarden_gpu.so; fi
     for w in ${WHAT:-M C3}; do run_one $v $w || { cp /tmp/lib_tree.so biogarden_amd/libbiogarden_gpu.so; exit 1; }; done
   done
 done
