@@ -130,8 +130,27 @@ __device__ __forceinline__ int dpp_shl1(int old, int src) {
 //     the consumer.  The caller stores it and loads the next incoming block.
 // Only the last strip, whose output row is row n1 (any lane), keeps the ring (score_chunk).
 // `mid` runs between the chunk's two halves (the kernel's HBM hand-offs).
+// The operand pipeline (codes 2 PF steps ahead, profile entries PF ahead) runs on across chunks:
+// a chunk's last steps prefetch the next chunk's first operands from the staged row (which holds
+// columns up to t0 + 127), so a chunk starts without a dependent code -> profile LDS round trip.
+constexpr int kConvPF = 4;
+template <int RW>
+struct ConvPipe {
+  int qCode[kConvPF];
+  ProfV<RW> qP[kConvPF];
+};
+// the strip's first chunk: operands of steps 0 .. PF - 1 and codes of steps PF .. 2 PF - 1
+template <int RW>
+__device__ __forceinline__ void conv_pipe_init(ConvPipe<RW>& pp, const TagCtx& C) {
+#pragma unroll
+  for (int d = 0; d < kConvPF; ++d) {
+    pp.qP[d] = load_prof<RW>(C.profLane + C.codeLane[d]);
+    pp.qCode[d] = C.codeLane[kConvPF + d];
+  }
+}
 template <int R, int VAR, class Mid>
-__device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C, int c, int& Q, Mid&& mid) {
+__device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C, int c, int& Q,
+                                                 ConvPipe<ProfW<R>::v>& pp, Mid&& mid) {
   const int a = C.a;
   const int lane = C.lane;
   constexpr int RW = ProfW<R>::v;
@@ -143,14 +162,9 @@ __device__ __forceinline__ void score_chunk_conv(TagStrip<R>& S, const TagCtx& C
       c0v[k] = wadd(col0_M(C.mode, i, a, C.b), -wmul(a, i));
     }
   }
-  constexpr int PF = 4;
-  int qCode[PF];
-  ProfV<RW> qP[PF];
-#pragma unroll
-  for (int d = 0; d < PF; ++d) {
-    qP[d] = load_prof<RW>(C.profLane + C.codeLane[d]);
-    qCode[d] = C.codeLane[PF + d];
-  }
+  constexpr int PF = kConvPF;
+  int (&qCode)[PF] = pp.qCode;
+  ProfV<RW> (&qP)[PF] = pp.qP;
   const uint16_t* cl = C.codeLane + 2 * PF;
 #pragma unroll
   for (int h = 0; h < BG_CHUNK / BG_TRACE_BLK; ++h, cl += BG_TRACE_BLK) {

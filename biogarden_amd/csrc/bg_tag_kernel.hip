@@ -385,6 +385,7 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
 #pragma unroll
       for (int k = 0; k <= R; ++k) { ckv[k] = 0; ckgv[k] = u32x2{0u, 0u}; }
       int Q = 0;
+      ConvPipe<RW> pipe;                                         // operands across chunks
       unsigned long long tData = 0, tFlow = 0;                   // BG_DEBUG=dp: spin cycles
       // LDS words read a boundary ahead (their latency hides behind the half's compute; the
       // words are monotonic, so a stale read only sends the wave down the polling path):
@@ -516,8 +517,9 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 1024) void bg_dp_tag_kernel(BgDpArg
           for (int k = 0; k <= R; ++k) asm volatile("" ::"v"(ckv[k]), "v"(ckgv[k].x), "v"(ckgv[k].y));
           boundary(2 * c + 1, gvB);
         };
-        if (c == 0 && !colMono) score_chunk_conv<R, TV_COL0>(S, C, c, Q, mid);
-        else score_chunk_conv<R, TV_FAST>(S, C, c, Q, mid);
+        if (c == 0) conv_pipe_init(pipe, C);
+        if (c == 0 && !colMono) score_chunk_conv<R, TV_COL0>(S, C, c, Q, pipe, mid);
+        else score_chunk_conv<R, TV_FAST>(S, C, c, Q, pipe, mid);
       }
       if (nh >= 1) emit(nh - 1, Q);                              // the last half: 2 NC - 3
       if (dbgOn && lane == 0) {
