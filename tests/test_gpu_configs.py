@@ -90,6 +90,23 @@ def test_C4_reads_vs_refs_slice(aligner, oracle):
     assert all(r.end[0] == 150 for r in res)
 
 
+def test_C4_rank0_share_as_benched(aligner, oracle):
+    """The 8 192-pair share the bench times (rank 0's LPT shard of the 65 536-read job over 8
+    GPUs, tools/configs.py C4): the grouped plan at full size, 48 sampled pairs string-exact."""
+    from biogarden_amd.shard import lpt_shards
+    w = _w()
+    allp = w.c4_pairs()
+    share = lpt_shards([(len(x), len(y)) for x, y in allp], 8)[0]
+    pairs = [allp[p] for p in share]
+    assert len(pairs) == 8192
+    res = check_batch(aligner, oracle, "semiglobal", pairs, "blosum62", -1, -2,
+                      sample=sample_indices(len(pairs), 48, 6))
+    st = aligner.stats()
+    assert st["tagged"] == 1 and st["checkpoint"] == 1 and st["group_pairs"] == 4 and st["R"] == 10, st
+    assert st["grouped"] == 2048, st
+    assert all(r.status == 0 and r.end[0] == 150 for r in res)
+
+
 def test_C5_protein_all_vs_all_share(aligner, oracle):
     w = _w()
     pairs = w.c5_pairs(rank=0, world=8)
