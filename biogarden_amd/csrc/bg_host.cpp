@@ -2476,7 +2476,7 @@ extern "C" int bg_batch_export_compact(bg_aligner* h, void* dst, size_t* bytes) 
     BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), xs));
     const unsigned g = (unsigned)(((uint64_t)E.nplan + 255) / 256);
     if (g) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(g), dim3(256), args, 0, xs));
-    BG_HIP(hipLaunchKernel(bg_compact_scan_kernel_ptr(), dim3(1), dim3(1024), args, 0, xs));
+    BG_HIP(hipLaunchKernel(bg_compact_scan_kernel_ptr(), dim3(1), dim3(64), args, 0, xs));
     BG_HIP(hipMemcpyAsync(&h->compactOps, E.sizes + n, 8, hipMemcpyDeviceToHost, xs));
     BG_HIP(hipStreamSynchronize(xs));
     h->compactExec = h->execCount;
@@ -2534,7 +2534,7 @@ extern "C" int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t ca
   BG_HIP(hipMemsetAsync(E.sizes, 0, 8 * (n + 1), xs));
   const unsigned gs = (unsigned)(((uint64_t)E.nplan + 255) / 256);
   if (gs) BG_HIP(hipLaunchKernel(bg_compact_size_kernel_ptr(), dim3(gs), dim3(256), args, 0, xs));
-  BG_HIP(hipLaunchKernel(bg_compact_scan_kernel_ptr(), dim3(1), dim3(1024), args, 0, xs));
+  BG_HIP(hipLaunchKernel(bg_compact_scan_kernel_ptr(), dim3(1), dim3(64), args, 0, xs));
   const unsigned gw = (unsigned)E.nplan + (unsigned)((n + 255) / 256) + 1;
   BG_HIP(hipLaunchKernel(bg_compact_write_kernel_ptr(), dim3(gw), dim3(256), args, 0, xs));
   BG_HIP(hipEventRecord(S.readDone, xs));

@@ -32,3 +32,32 @@ __global__ __launch_bounds__(256) void bg_download_kernel(BgDownloadArgs A) {
 }
 
 extern "C" void* bg_download_kernel_ptr() { return (void*)&bg_download_kernel; }
+
+// Exclusive scan of the compact record's caller-order sizes (bg_batch_export_compact): ONE wave,
+// a chunk per lane, then a shuffle scan; sizes[n] = the total.  One wave fits on a CU beside the
+// next execute's DP workgroup and its tracebacks.  (The first form was one 1024-thread workgroup
+// scanning its partial sums in one thread: it found no CU until the DP beside it ended, and on the
+// pipelined group's path every third DP then waited ~1 ms for the collect behind it.)
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int o) {
+  const unsigned lo = __shfl_up((unsigned)v, o, 64), hi = __shfl_up((unsigned)(v >> 32), o, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__global__ __launch_bounds__(64) void bg_compact_scan_kernel(BgCompactArgs E) {
+  const uint64_t n = E.npairs_caller;
+  const unsigned lane = threadIdx.x;
+  const uint64_t per = (n + 63) / 64;
+  const uint64_t lo = lane * per, hi = lo + per < n ? lo + per : n;
+  uint64_t s = 0;
+  for (uint64_t p = lo; p < hi; ++p) s += E.sizes[p];
+  uint64_t x = s;                                         // inclusive scan over the wave
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t y = shfl_up_u64(x, o);
+    if ((int)lane >= o) x += y;
+  }
+  if (lane == 63) E.sizes[n] = x;
+  uint64_t acc = x - s;                                   // this lane's chunk starts here
+  for (uint64_t p = lo; p < hi; ++p) { const uint64_t v = E.sizes[p]; E.sizes[p] = acc; acc += v; }
+}
+
+extern "C" void* bg_compact_scan_kernel_ptr() { return (void*)&bg_compact_scan_kernel; }

@@ -481,25 +481,6 @@ __global__ __launch_bounds__(256) void bg_compact_size_kernel(BgCompactArgs E) {
   E.sizes[P.caller] = (ncore + 3) / 4;
 }
 
-__global__ __launch_bounds__(1024) void bg_compact_scan_kernel(BgCompactArgs E) {
-  __shared__ uint64_t part[1024];
-  const uint64_t n = E.npairs_caller;
-  const uint64_t per = (n + blockDim.x - 1) / blockDim.x;
-  const uint64_t lo = threadIdx.x * per, hi = lo + per < n ? lo + per : n;
-  uint64_t s = 0;
-  for (uint64_t p = lo; p < hi; ++p) s += E.sizes[p];
-  part[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t acc = 0;
-    for (unsigned t = 0; t < blockDim.x; ++t) { const uint64_t v = part[t]; part[t] = acc; acc += v; }
-    E.sizes[n] = acc;
-  }
-  __syncthreads();
-  uint64_t acc = part[threadIdx.x];
-  for (uint64_t p = lo; p < hi; ++p) { const uint64_t v = E.sizes[p]; E.sizes[p] = acc; acc += v; }
-}
-
 __global__ __launch_bounds__(256) void bg_compact_write_kernel(BgCompactArgs E) {
   uint64_t* head = reinterpret_cast<uint64_t*>(E.dst);
   BgCompactHdr* hdr = reinterpret_cast<BgCompactHdr*>(E.dst + 32);
@@ -536,7 +517,6 @@ __global__ __launch_bounds__(256) void bg_compact_write_kernel(BgCompactArgs E) 
 }
 
 extern "C" void* bg_compact_size_kernel_ptr() { return (void*)&bg_compact_size_kernel; }
-extern "C" void* bg_compact_scan_kernel_ptr() { return (void*)&bg_compact_scan_kernel; }
 extern "C" void* bg_compact_write_kernel_ptr() { return (void*)&bg_compact_write_kernel; }
 
 // Residue coding on the device: codes[x] = lut[raw[x]] over both concatenated sequence sets
