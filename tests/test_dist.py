@@ -35,8 +35,8 @@ def _pairs(n, seed):
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
         pairs = _pairs(23, 7)
         shards = shard.lpt_shards([(len(a), len(b)) for a, b in pairs], world)
         mine = [pairs[p] for p in shards[rank]]
@@ -52,7 +52,8 @@ def _worker(rank, world, port, q):
         q.put(("err", repr(e)))
         raise
     finally:
-        dist.destroy_process_group()
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
 
 def _oracle_results(pairs, mode, a, b):
@@ -87,8 +88,8 @@ def _sharded_worker(rank, world, port, q, mode, a, b):
     the caller's pair order."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
         pairs = _real_pairs(37, 11)
         shards = shard.lpt_shards([(len(x), len(y)) for x, y in pairs], world)
         mine = _oracle_results([pairs[p] for p in shards[rank]], mode, a, b)
@@ -104,7 +105,8 @@ def _sharded_worker(rank, world, port, q, mode, a, b):
         q.put(("err", repr(e)))
         raise
     finally:
-        dist.destroy_process_group()
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
 
 def _faithful_results(pairs, mode, a, b, dims):
@@ -143,8 +145,8 @@ def _c4_sharded_worker(rank, world, port, q):
     """A C4-shaped batch through the multi-rank path with the whole batch's call history."""
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
         mode, a, b = "semiglobal", -1, -2
         pairs = _c4_like_pairs()
         sizes = [(len(x), len(y)) for x, y in pairs]
@@ -172,7 +174,8 @@ def _c4_sharded_worker(rank, world, port, q):
         q.put(("err", repr(e)))
         raise
     finally:
-        dist.destroy_process_group()
+        if dist.is_initialized():
+            dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -181,15 +184,7 @@ def test_c4_shaped_shards_equal_one_reference_aligner(world):
     batch's scratch history: merged statuses, scores and strings equal ONE reference aligner
     running the batch in order (status 4 exactly where that aligner panics or answers from
     stale scratch)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_c4_sharded_worker, args=(r, world, port, q)) for r in range(world)]
-    for p in procs:
-        p.start()
-    msgs = [q.get(timeout=300) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=120)
+    msgs, procs = _run_world(_c4_sharded_worker, world, timeout=300)
     ok = [m for m in msgs if m[0] == "ok"]
     assert len(ok) == 1, msgs
     _, same, statuses, seq, scores, strings = ok[0]
@@ -207,16 +202,7 @@ def test_c4_shaped_shards_equal_one_reference_aligner(world):
 def test_sharded_batch_equals_single_rank(world):
     """The multi-rank data path on CPU ranks: the merged gather of every rank's packed shard
     equals a single-rank run of the same pairs, pair for pair (status, score, both strings)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_sharded_worker, args=(r, world, port, q, "semiglobal", -11, -1))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    msgs = [q.get(timeout=180) for _ in range(world)]
-    for p in procs:
-        p.join(timeout=120)
+    msgs, procs = _run_world(_sharded_worker, world, ("semiglobal", -11, -1))
     ok = [m for m in msgs if m[0] == "ok"]
     assert len(ok) == 1, msgs
     assert ok[0][1] and ok[0][2] == 37 and min(ok[0][3]) > 0, ok
@@ -228,6 +214,34 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _run_world(target, world, extra=(), nmsgs=None, timeout=180):
+    """Spawns `world` gloo ranks of target(rank, world, port, q, *extra) and returns (messages,
+    processes).  A port taken between _free_port and the store's bind (another process on the
+    machine) fails rank 0's init with EADDRINUSE: that try is torn down and run again on a fresh
+    port, at most three times."""
+    ctx = mp.get_context("spawn")
+    nmsgs = world if nmsgs is None else nmsgs
+    for attempt in range(3):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=target, args=(r, world, port, q) + tuple(extra)) for r in range(world)]
+        for p in procs:
+            p.start()
+        msgs = []
+        while len(msgs) < nmsgs:
+            msgs.append(q.get(timeout=timeout))
+            if msgs[-1][0] == "err" and "EADDRINUSE" in msgs[-1][1] and attempt < 2:
+                break
+        else:
+            for p in procs:
+                p.join(timeout=120)
+            return msgs, procs
+        for p in procs:
+            p.kill()
+            p.join(timeout=30)
+    raise AssertionError("unreachable")
 
 
 def test_lpt_shards_balance_and_cover():
@@ -245,15 +259,7 @@ def test_encode_decode_roundtrip():
 
 
 def test_gather_two_ranks_gloo():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    msg = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=120)
+    (msg,), procs = _run_world(_worker, 2, nmsgs=1, timeout=120)
     assert msg[0] == "ok", msg
     assert msg[1] and msg[2] == 23 and msg[3]
     assert all(p.exitcode == 0 for p in procs)
