@@ -20,8 +20,9 @@
 // Members on one device share that device's HIP streams (bg_aligner_new_shared), so their DPs and
 // tracebacks pipeline as consecutive executes of one handle do.
 // bg_group_submit / bg_group_collect split a call in two so that kGSlots batches are in flight:
-// every member has kGSlots aligners (pipeline slots), a submit runs steps 1-3 up to the executes
-// and returns, a collect runs the exports, 4 and 5 of the oldest batch.  Three: while the host
+// every member has kGSlots aligners (pipeline slots), a submit runs steps 1-3 (each member's
+// compact export queued on its traceback's stream right behind it) and returns, a collect runs 4
+// and 5 of the oldest batch on the download streams, which wait for that batch's exports only.  Three: while the host
 // collects batch k (its traceback, then ~1 ms of expansion), k + 1 and k + 2 keep the device's
 // DP stream busy (two left it idle for the expansion: M 6 500 GCUPS against 4 608 synchronous).  While one batch's DPs and
 // tracebacks run on the devices, the host prepares the next and expands the previous, and the
@@ -50,6 +51,8 @@
 #include "biogarden_gpu.h"
 
 extern "C" void* bg_aligner_aux_stream(bg_aligner* h);   // bg_host.cpp
+extern "C" int bg_batch_export_compact_behind_traceback(bg_aligner* h, void* dst, size_t cap,
+                                                         void* first, void* done);   // bg_host.cpp
 extern "C" void* bg_download_kernel_ptr();                // bg_io.hip
 
 namespace {
@@ -109,6 +112,7 @@ struct GBatch {
   std::vector<uint64_t> coff;
   uint64_t need = 0;
   std::vector<std::vector<size_t>> idx;   // member -> its pairs (caller indices)
+  std::vector<size_t> size;               // member -> its compact record's bound (bytes)
 };
 
 struct bg_group {
@@ -121,6 +125,8 @@ struct bg_group {
                                    // stream, owned by the members' aligners)
   std::vector<void*> ebuf;         // (member, slot) -> its compact record (on its device)
   std::vector<size_t> ecap;
+  std::vector<hipEvent_t> xev;     // (member, slot) -> its record written (traceback stream)
+  std::vector<hipEvent_t> sev;     // (member, slot) -> its record read by the gather (on cs)
   std::deque<GBatch> pending;      // submitted, not yet collected (at most kGSlots)
   int nextSlot = 0;
   void* gbuf = nullptr;            // the gathered records, on the root device
@@ -151,6 +157,11 @@ extern "C" void bg_group_free(bg_group* g) {
     if (g->comm[r]) (void)rccl().commDestroy(g->comm[r]);
   for (size_t x = 0; x < g->ebuf.size(); ++x)
     if (g->ebuf[x]) { (void)hipSetDevice(g->dev[x / kGSlots]); (void)hipFree(g->ebuf[x]); }
+  for (size_t x = 0; x < g->xev.size(); ++x) {
+    (void)hipSetDevice(g->dev[x / kGSlots]);
+    if (g->xev[x]) (void)hipEventDestroy(g->xev[x]);
+    if (g->sev[x]) (void)hipEventDestroy(g->sev[x]);
+  }
   if (g->gbuf) { (void)hipSetDevice(g->rankDev[0]); (void)hipFree(g->gbuf); }
   if (g->hbuf) (void)hipHostFree(g->hbuf);
   // members sharing a device's streams: the stream owner (the first on its device) goes last
@@ -197,6 +208,15 @@ extern "C" bg_group* bg_group_new(const int* devices, int n) {
     g->cs[r] = static_cast<hipStream_t>(bg_aligner_aux_stream(g->h[kGSlots * first]));
     if (!g->cs[r]) { bg_group_free(g); return nullptr; }
   }
+  g->xev.assign(kGSlots * n, nullptr);
+  g->sev.assign(kGSlots * n, nullptr);
+  for (int x = 0; x < kGSlots * n; ++x)
+    if (hipSetDevice(g->dev[x / kGSlots]) != hipSuccess ||
+        hipEventCreateWithFlags(&g->xev[x], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&g->sev[x], hipEventDisableTiming) != hipSuccess) {
+      bg_group_free(g);
+      return nullptr;
+    }
   const ncclResult_t rc = rccl().commInitAll(g->comm.data(), nr, g->rankDev.data());
   if (rc != ncclSuccess) {
     nccl_fail(rc, "ncclCommInitAll");
@@ -297,11 +317,35 @@ extern "C" int bg_group_submit(bg_group* g, int mode, size_t npairs, const uint8
   }
   for (int m = 0; m < M; ++m)
     if (rc[m]) return rc[m];
+  g->ms[kGPrepExec] += ms_since(t);
+  // 3 (second half): every member's compact export, queued without a host wait on its traceback's
+  // stream right behind it, into its slot's buffer (sized by the record's bound) once the gather of
+  // the slot's previous batch has read it (sev); xev marks it written
+  B.size.assign(M, 0);
+  for (int m = 0; m < M; ++m) {
+    if (B.idx[m].empty()) continue;
+    const int x = kGSlots * m + B.slot;
+    bg_aligner* h = g->h[x];
+    size_t sz = 0;
+    int e = bg_batch_export_compact_bound(h, &sz);
+    hipError_t he = hipSetDevice(g->dev[m]);
+    if (!e && he != hipSuccess) e = hip_fail(he, "hipSetDevice");
+    if (!e && g->ecap[x] < sz) {
+      if (g->ebuf[x]) (void)hipFree(g->ebuf[x]);
+      g->ebuf[x] = nullptr;
+      g->ecap[x] = 0;
+      if (hipMalloc(&g->ebuf[x], sz + sz / 4) != hipSuccess) { g->ebuf[x] = nullptr; e = BG_E_NOMEM; }
+      else g->ecap[x] = sz + sz / 4;
+    }
+    if (!e) e = bg_batch_export_compact_behind_traceback(h, g->ebuf[x], sz, g->sev[x], g->xev[x]);
+    if (e) return e;
+    B.size[m] = sz;
+  }
   g->rows = rows;
   g->cols = cols;
   g->nextSlot = (g->nextSlot + 1) % kGSlots;
   g->pending.push_back(std::move(B));
-  g->ms[kGPrepExec] += ms_since(t);
+  g->ms[kGExport] += ms_since(t);
   return BG_OK;
 }
 
@@ -314,36 +358,11 @@ extern "C" int bg_group_collect(bg_group* g, bg_pair_result* res, uint8_t* out1,
   auto t = std::chrono::steady_clock::now();
   ++g->calls;
   const int M = (int)g->dev.size();
-  // 3 (second half): every member's compact export, queued without a host wait
-  // (bg_batch_export_compact_async) on its device's download stream behind the batch's traceback,
-  // into a buffer sized by the record's bound; the gather and the download below follow on the
-  // same streams, so the host waits once per collect, for the download
-  std::vector<size_t> size(M, 0);
-  int err = BG_OK;
-  for (int m = 0; m < M && !err; ++m) {
-    if (B.idx[m].empty()) continue;
-    const int x = kGSlots * m + B.slot;
-    bg_aligner* h = g->h[x];
-    size_t sz = 0;
-    int e = bg_batch_export_compact_bound(h, &sz);
-    if (!e && g->ecap[x] < sz) {
-      (void)hipSetDevice(g->dev[m]);
-      if (g->ebuf[x]) (void)hipFree(g->ebuf[x]);
-      g->ebuf[x] = nullptr;
-      g->ecap[x] = 0;
-      if (hipMalloc(&g->ebuf[x], sz + sz / 4) != hipSuccess) { g->ebuf[x] = nullptr; e = BG_E_NOMEM; }
-      else g->ecap[x] = sz + sz / 4;
-    }
-    if (!e) e = bg_batch_export_compact_async(h, g->ebuf[x], sz, g->cs[g->rankOf[m]]);
-    size[m] = sz;
-    err = e;
-  }
+  const std::vector<size_t>& size = B.size;
   auto finish = [&](int e) {
     g->pending.pop_front();
     return e;
   };
-  if (err) return finish(err);
-  g->ms[kGExport] += ms_since(t);
   // 4: the gather into one buffer on the root device
   std::vector<uint64_t> goff(M + 1, 0);
   for (int m = 0; m < M; ++m) goff[m + 1] = goff[m] + size[m];
@@ -361,11 +380,20 @@ extern "C" int bg_group_collect(bg_group* g, bg_pair_result* res, uint8_t* out1,
   bool viaRccl = false;
   for (int m = 0; m < M; ++m)
     if (size[m] && (g->rankOf[m] != 0 || g->rcclSelf)) viaRccl = true;
+  // every gather stream waits for the records it reads (this batch's exports, xev)
+  for (int m = 0; m < M; ++m) {
+    if (!size[m]) continue;
+    const int r = g->rankOf[m];
+    if ((he = hipSetDevice(g->rankDev[r])) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
+    if ((he = hipStreamWaitEvent(g->cs[r], g->xev[kGSlots * m + B.slot], 0)) != hipSuccess)
+      return finish(hip_fail(he, "wait export"));
+  }
   for (int m = 0; m < M; ++m)
     if (size[m] && g->rankOf[m] == 0 && !g->rcclSelf) {
       if ((he = hipSetDevice(root)) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
       if ((he = hipMemcpyAsync(gb + goff[m], g->ebuf[kGSlots * m + B.slot], size[m], hipMemcpyDeviceToDevice,
-                               g->cs[0])) != hipSuccess)
+                               g->cs[0])) != hipSuccess ||
+          (he = hipEventRecord(g->sev[kGSlots * m + B.slot], g->cs[0])) != hipSuccess)
         return finish(hip_fail(he, "gather copy"));
     }
   if (viaRccl) {
@@ -383,9 +411,16 @@ extern "C" int bg_group_collect(bg_group* g, bg_pair_result* res, uint8_t* out1,
     const ncclResult_t ne = R.groupEnd();
     if (nr != ncclSuccess) return finish(nccl_fail(nr, "ncclSend / ncclRecv"));
     if (ne != ncclSuccess) return finish(nccl_fail(ne, "ncclGroupEnd"));
+    // the slot's next export waits for the send that reads its buffer (sev)
+    for (int m = 0; m < M; ++m) {
+      if (!size[m] || (g->rankOf[m] == 0 && !g->rcclSelf)) continue;
+      const int r = g->rankOf[m];
+      if ((he = hipSetDevice(g->rankDev[r])) != hipSuccess ||
+          (he = hipEventRecord(g->sev[kGSlots * m + B.slot], g->cs[r])) != hipSuccess)
+        return finish(hip_fail(he, "record send"));
+    }
   }
-  // (no host wait: the download below is queued behind the receives on the root's stream, and a
-  // sender's next export waits for its slot's readDone, which follows the send on that stream)
+  // (no host wait: the download below is queued behind the receives on the root's stream)
   if ((he = hipSetDevice(root)) != hipSuccess) return finish(hip_fail(he, "hipSetDevice"));
   g->ms[kGGather] += ms_since(t);
   // 5: one download, then the expansion into the caller's buffers at the caller's offsets.  The

@@ -248,6 +248,7 @@ struct bg_aligner {
   hipStream_t dps = nullptr;
   hipStream_t upS = nullptr;       // shared handles: uploads (a queue of their own)
   hipStream_t dlS = nullptr;       // downloads of the asynchronous fetch (bg_set_async_fetch)
+  hipStream_t lastFs = nullptr;    // the stream the last execute's traceback ran on
   // bg_set_async_fetch: every execute queues its results' download (into ho1 / ho2 / hresPin)
   // right after its traceback; bg_batch_fetch then only waits for it and unpacks
   int asyncFetch = 0;
@@ -2031,6 +2032,7 @@ extern "C" int bg_batch_execute(bg_aligner* h) {
   exMark("finish");
   BG_HIP(hipEventRecord(e[3], fs));
   BG_HIP(hipEventRecord(S.finDone, fs));
+  h->lastFs = fs;
   S.inflight = true;
   S.dpPending = false;
   exMark("fin-events");
@@ -2508,16 +2510,12 @@ extern "C" int bg_batch_export_compact_bound(bg_aligner* h, size_t* bytes) {
 // last execute's traceback; the slot's next execute waits for them (readDone), and `after` (a
 // stream of the handle's device; null = its null stream) waits for them too, so a collective
 // queued there reads a finished record.
-extern "C" int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t cap, void* after) {
-  if (!h || !dst) return BG_E_ARG;
-  if (!h->prepared || !h->executed) return BG_E_NO_BATCH;
+// the size, scan and write kernels of the last execute's compact record, queued on xs behind its
+// traceback; the slot's next execute waits for them (readDone)
+static int export_compact_queue(bg_aligner* h, void* dst, size_t cap, hipStream_t xs) {
   const uint64_t n = h->npairs;
   if (cap < 32 + n * sizeof(bg_compact_hdr) + h->opsBytes) return BG_E_ARG;
-  BG_HIP(hipSetDevice(h->device));
   Slot& S = h->slot[h->lastSlot];
-  if (!h->dlS) h->dlS = group_stream(h, kSDl);
-  if (!h->dlS) return BG_E_HIP;
-  hipStream_t xs = h->dlS;
   if (!h->compactSizes.ensure(8 * (n + 1))) return BG_E_NOMEM;
   BgCompactArgs E;
   E.pairs = h->pairs.as<BgPair>();
@@ -2540,8 +2538,36 @@ extern "C" int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t ca
   BG_HIP(hipEventRecord(S.readDone, xs));
   S.readPending = true;
   h->compactExec = -1;             // the sizes now belong to this record
+  return BG_OK;
+}
+
+extern "C" int bg_batch_export_compact_async(bg_aligner* h, void* dst, size_t cap, void* after) {
+  if (!h || !dst) return BG_E_ARG;
+  if (!h->prepared || !h->executed) return BG_E_NO_BATCH;
+  BG_HIP(hipSetDevice(h->device));
+  if (!h->dlS) h->dlS = group_stream(h, kSDl);
+  if (!h->dlS) return BG_E_HIP;
+  const int e = export_compact_queue(h, dst, cap, h->dlS);
+  if (e) return e;
   // NULL is the device's null stream (torch's default current stream): a valid stream to order
-  BG_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(after), S.readDone, 0));
+  BG_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(after), h->slot[h->lastSlot].readDone, 0));
+  return BG_OK;
+}
+
+// bg_group's form (not in the C ABI): the record is queued on the traceback's own stream right
+// after the execute, once `first` (the previous reader of dst) has fired, and `done` marks it
+// written.  On the download stream the exports of the batches in flight would sit ahead of the
+// oldest batch's gather and download, and each waits for its own traceback.
+extern "C" int bg_batch_export_compact_behind_traceback(bg_aligner* h, void* dst, size_t cap,
+                                                         void* first, void* done) {
+  if (!h || !dst || !done) return BG_E_ARG;
+  if (!h->prepared || !h->executed) return BG_E_NO_BATCH;
+  BG_HIP(hipSetDevice(h->device));
+  hipStream_t xs = h->lastFs ? h->lastFs : h->stream2;
+  if (first) BG_HIP(hipStreamWaitEvent(xs, static_cast<hipEvent_t>(first), 0));
+  const int e = export_compact_queue(h, dst, cap, xs);
+  if (e) return e;
+  BG_HIP(hipEventRecord(static_cast<hipEvent_t>(done), xs));
   return BG_OK;
 }
 
